@@ -1,0 +1,112 @@
+"""ctypes binding of include/dbsde.h (the C ABI of the HIP library).
+
+The library is built in-tree by __graft_entry__.build() / build_lib.py into
+lib/libdbsde.so.  There is no fallback: if the library (or a GPU) is missing,
+every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libdbsde.so")
+
+DBSDE_OK, DBSDE_EINVAL, DBSDE_EHIP, DBSDE_ENOMEM = 0, -1, -2, -3
+
+MODES = {"FC": 0, "NAIS-Net": 1, "Resnet": 2, "Naisnet": 3}
+ACTIVATIONS = {"Sine": 0, "ReLU": 1, "Tanh": 2}
+G_KINDS = {"sumsq": 0, "call_sum": 1, "call_mean": 2, "log": 3}
+OPTIMIZERS = {"Adam": 0, "AdamW": 1, "SGD": 2}
+
+# every symbol include/dbsde.h declares (checked by the CPU test suite)
+EXPORTED = [
+    "dbsde_abi_version", "dbsde_create", "dbsde_destroy", "dbsde_last_error", "dbsde_set_stream",
+    "dbsde_param_count", "dbsde_param_used_mask", "dbsde_loss_grad", "dbsde_net_u",
+    "dbsde_optimizer_step", "dbsde_profile_enable", "dbsde_profile_count", "dbsde_profile_read",
+    "dbsde_profile_reset",
+]
+
+
+class Problem(ctypes.Structure):
+    _fields_ = [("mu_a", ctypes.c_float), ("sig_a", ctypes.c_float), ("sig_b", ctypes.c_float),
+                ("phi_r", ctypes.c_float), ("phi_c", ctypes.c_float), ("phi_zz", ctypes.c_float),
+                ("g_kind", ctypes.c_int), ("strike", ctypes.c_float), ("q3", ctypes.c_int)]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("activation", ctypes.c_int), ("n_layers", ctypes.c_int),
+                ("layers", ctypes.c_int * 16), ("problem", Problem), ("T", ctypes.c_float),
+                ("device", ctypes.c_int)]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("M", ctypes.c_int), ("N", ctypes.c_int), ("t", ctypes.c_void_p), ("W", ctypes.c_void_p),
+                ("seed", ctypes.c_ulonglong), ("offset", ctypes.c_ulonglong), ("path0", ctypes.c_longlong),
+                ("Xi", ctypes.c_void_p),
+                ("xi_rows", ctypes.c_int)]
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [("loss", ctypes.c_void_p), ("X", ctypes.c_void_p), ("Y", ctypes.c_void_p),
+                ("Z", ctypes.c_void_p)]
+
+
+class Optim(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
+                ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
+                ("max_norm", ctypes.c_float), ("step", ctypes.c_longlong)]
+
+
+_LIB = None
+
+
+def load():
+    """Load lib/libdbsde.so (no HIP call is made by loading)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build the HIP library first (python __graft_entry__.py build)")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, i, ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_longlong
+    sig = {
+        "dbsde_abi_version": (i, []),
+        "dbsde_create": (i, [ctypes.POINTER(Config), ctypes.POINTER(vp)]),
+        "dbsde_destroy": (None, [vp]),
+        "dbsde_last_error": (ctypes.c_char_p, [vp]),
+        "dbsde_set_stream": (i, [vp, vp]),
+        "dbsde_param_count": (ll, [vp]),
+        "dbsde_param_used_mask": (i, [vp, vp, ll]),
+        "dbsde_loss_grad": (i, [vp, vp, ctypes.POINTER(Batch), vp, ctypes.POINTER(Outputs)]),
+        "dbsde_net_u": (i, [vp, vp, i, vp, vp, vp, vp]),
+        "dbsde_optimizer_step": (i, [vp, vp, vp, vp, vp, ctypes.POINTER(Optim)]),
+        "dbsde_profile_enable": (i, [vp, i]),
+        "dbsde_profile_count": (i, [vp]),
+        "dbsde_profile_read": (i, [vp, i, ctypes.c_char_p, i, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ll)]),
+        "dbsde_profile_reset": (i, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.dbsde_abi_version() != 1:
+        raise RuntimeError("libdbsde ABI version mismatch")
+    _LIB = lib
+    return lib
+
+
+def check(rc, ctx=None):
+    """Map a C status to the reference's Python exception types."""
+    if rc == DBSDE_OK:
+        return
+    msg = load().dbsde_last_error(ctx)
+    msg = msg.decode() if msg else "unknown error"
+    if rc == DBSDE_EINVAL:
+        raise ValueError(msg)
+    if rc == DBSDE_ENOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(msg)

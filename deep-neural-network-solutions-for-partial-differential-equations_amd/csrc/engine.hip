@@ -1,0 +1,1158 @@
+// engine.hip -- context, buffers and launch sequence of the deep-BSDE step,
+// exported through the C ABI of include/dbsde.h.
+//
+// One dbsde_loss_grad call = FBSNN.loss_function + loss.backward of the
+// reference (DeepBSDE.py:202-245, 279) restated time-parallel:
+//   prep      NAIS projection A_j (Q4), weight packing       (once per call)
+//   rollout   Euler-Maruyama X path, sigma*dW                 (HBM-bound)
+//   forward   x-stack GEMM + K block GEMMs, u                 (MFMA fp32)
+//   input-grad K block GEMMs + Z GEMM with the residual epilogue
+//   tangent   forward-mode along zbar                         (MFMA fp32)
+//   reverse   K block GEMMs                                   (MFMA fp32)
+//   weight-grad split-K TN GEMMs into slabs, fixed-order slab sums, NAIS adjoint
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/dbsde.h"
+#include "kernels.hpp"
+
+using namespace dbsde;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+constexpr int TN_SPLITS = 32;   // fixed split count -> static slab layout
+constexpr int OUT_SPLITS = 64;  // output-layer column-sum splits
+
+inline int pad16(int x) { return (x + 15) / 16 * 16; }
+inline int padw(int x) { return x <= 128 ? pad16(x) : (x + 127) / 128 * 128; }
+inline int nt_for(int w) { return w <= 128 ? w / 16 : 8; }
+
+struct Lin {
+  long long w = -1, b = -1;
+  int out = 0, in = 0;
+};
+
+struct ProfAgg {
+  std::string name;
+  double ms = 0, flops = 0, bytes = 0;
+  long long n = 0;
+};
+struct ProfRec {
+  int id;
+  hipEvent_t e0, e1;
+  double flops, bytes;
+};
+
+}  // namespace
+
+struct dbsde_ctx {
+  dbsde_config cfg{};
+  std::string err;
+  hipStream_t stream = nullptr;
+  int device = 0;
+
+  // ---- network description
+  int mode = 0, act = 0, K = 0, D = 0;
+  std::vector<int> L;
+  bool has_v = false, proj = false;
+  float rho = 0.f;
+  Lin in, out;
+  std::vector<Lin> B, V;  // B[j-1], V[j-1] for block j = 1..K
+  long long nparams = 0;
+  std::vector<unsigned char> used;
+
+  // ---- padded geometry
+  int Dp = 0, Stot = 0, Stot_x = 0, Wmax = 0;
+  std::vector<int> Wp, col;  // per level j = 0..K
+
+  // ---- weight buffers (fixed)
+  float *BtIn = nullptr, *BtZ = nullptr, *wout = nullptr, *bout = nullptr;
+  std::vector<float*> Bf, Bb, beta, rtr, abar;
+  double* norms = nullptr;
+  long long* d_woffs = nullptr;   // NAIS: W_j offsets in the flat params
+  float** d_rtr = nullptr;
+  float** d_abar = nullptr;
+  unsigned char* d_used = nullptr;
+  PackDesc* d_prep = nullptr;
+  int n_prep = 0;
+  PackDesc* d_fin = nullptr;
+  int n_fin = 0;
+  std::vector<float*> slab;  // TN problem slabs (0 = x-stack, j = block j)
+  std::vector<int> slab_mt, slab_nt;
+  float* out_slab = nullptr;
+  int out_ld = 0;
+  double* opt_part = nullptr;
+  int opt_nparts = 0;
+
+  // ---- row buffers (grow with Rp)
+  int cap_rows = 0, cap_n = 0;
+  float *xin = nullptr, *sdw = nullptr, *zbar = nullptr, *zfull = nullptr;
+  float *Abuf = nullptr, *Adot = nullptr, *Delta = nullptr, *Alpha = nullptr, *H = nullptr, *Hdot = nullptr,
+        *G = nullptr;
+  float* Pbuf[2] = {nullptr, nullptr};
+  float *u = nullptr, *rres = nullptr, *lossrow = nullptr, *ubar = nullptr, *q3S = nullptr;
+  double* loss_part = nullptr;
+  float* loss_tmp = nullptr;
+
+  std::vector<void*> allocs;      // fixed-size buffers
+  std::vector<void*> row_allocs;  // buffers sized by the row count (regrown)
+
+  // ---- profiling
+  bool prof = false;
+  std::vector<ProfAgg> agg;
+  std::map<std::string, int> agg_idx;
+  std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> ev_pool;
+};
+
+namespace {
+
+int fail(dbsde_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  g_last_error = msg;
+  return code;
+}
+
+#define HIPC(ctx, expr)                                                                         \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return fail(ctx, DBSDE_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+  } while (0)
+
+int dalloc(dbsde_ctx* c, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return fail(c, DBSDE_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  e = hipMemset(*p, 0, bytes);
+  if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("hipMemset: ") + hipGetErrorString(e));
+  c->allocs.push_back(*p);
+  return DBSDE_OK;
+}
+template <typename T>
+int dalloc_t(dbsde_ctx* c, T** p, size_t n) {
+  return dalloc(c, (void**)p, n * sizeof(T));
+}
+
+hipEvent_t get_event(dbsde_ctx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+int prof_id(dbsde_ctx* c, const std::string& name) {
+  auto it = c->agg_idx.find(name);
+  if (it != c->agg_idx.end()) return it->second;
+  int id = (int)c->agg.size();
+  c->agg.push_back(ProfAgg{name});
+  c->agg_idx[name] = id;
+  return id;
+}
+
+// Launch wrapper: per-kernel HIP events when profiling is on.
+template <typename F>
+int run(dbsde_ctx* c, const char* name, double flops, double bytes, F&& launch) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->prof) {
+    e0 = get_event(c);
+    e1 = get_event(c);
+    if (e0) (void)hipEventRecord(e0, c->stream);
+  }
+  launch();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string(name) + ": " + hipGetErrorString(e));
+  if (c->prof && e0 && e1) {
+    (void)hipEventRecord(e1, c->stream);
+    c->pending.push_back(ProfRec{prof_id(c, name), e0, e1, flops, bytes});
+  }
+  return DBSDE_OK;
+}
+
+#define RUN(ctx, name, fl, by, ...)                        \
+  do {                                                     \
+    int rc_ = run(ctx, name, fl, by, [&]() { __VA_ARGS__; }); \
+    if (rc_) return rc_;                                   \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// network layout (state_dict order; oracle/timeparallel.param_layout mirrors it)
+// ---------------------------------------------------------------------------
+int build_net(dbsde_ctx* c) {
+  const dbsde_config& g = c->cfg;
+  if (g.n_layers < 4 || g.n_layers > 16) return fail(c, DBSDE_EINVAL, "len(layers) must be in [4, 16]");
+  c->L.assign(g.layers, g.layers + g.n_layers);
+  for (int v : c->L)
+    if (v <= 0) return fail(c, DBSDE_EINVAL, "layer widths must be positive");
+  const int n = g.n_layers;
+  c->D = c->L[0] - 1;
+  if (c->L.back() != 1) return fail(c, DBSDE_EINVAL, "last layer width must be 1 (u is a scalar)");
+  if (c->D < 1) return fail(c, DBSDE_EINVAL, "layers[0] must be D+1 >= 2");
+  c->K = n - 3;
+  c->mode = g.mode;
+  c->act = g.activation;
+  if (c->act < 0 || c->act > 2) return fail(c, DBSDE_EINVAL, "unknown activation");
+  long long off = 0;
+  auto lin = [&](int o, int i) {
+    Lin l;
+    l.out = o;
+    l.in = i;
+    l.w = off;
+    off += (long long)o * i;
+    l.b = off;
+    off += o;
+    return l;
+  };
+  c->B.clear();
+  c->V.clear();
+  const auto& L = c->L;
+  if (g.mode == DBSDE_MODE_FC) {
+    c->has_v = false;
+    c->proj = false;
+    c->rho = 0.f;
+    c->in = lin(L[1], L[0]);
+    for (int j = 1; j <= c->K; ++j) c->B.push_back(lin(L[j + 1], L[j]));
+    c->out = lin(L[n - 1], L[n - 2]);
+  } else if (g.mode == DBSDE_MODE_NAIS_NET || g.mode == DBSDE_MODE_RESNET) {
+    const bool st = g.mode == DBSDE_MODE_NAIS_NET;
+    c->has_v = st;
+    c->proj = st;
+    c->rho = 1.f;
+    c->in = lin(L[1], L[0]);
+    for (int j = 1; j <= c->K; ++j) c->B.push_back(lin(L[j + 1], L[j]));
+    c->out = lin(L[n - 1], L[n - 2]);
+    if (st)
+      for (int i = 1; i <= n - 2; ++i) {
+        Lin v = lin(L[i], L[0]);
+        if (i <= c->K) c->V.push_back(v);  // input_layers[K] is never used (Q6)
+      }
+  } else if (g.mode == DBSDE_MODE_NAISNET) {
+    if (n < 4 || n > 6) return fail(c, DBSDE_EINVAL, "Naisnet supports len(layers) in {4,5,6}");
+    c->has_v = true;
+    c->proj = true;
+    c->rho = 1.f;
+    c->in = lin(L[1], L[0]);
+    for (int j = 1; j <= c->K; ++j) {
+      c->B.push_back(lin(L[j + 1], L[j]));
+      c->V.push_back(lin(L[j + 1], L[0]));
+    }
+    c->out = lin(L[n - 1], L[n - 2]);
+  } else {
+    return fail(c, DBSDE_EINVAL, "unknown mode");
+  }
+  if (c->rho != 0.f)
+    for (int j = 2; j < n - 1; ++j)
+      if (L[j] != L[1]) return fail(c, DBSDE_EINVAL, "residual modes need equal hidden widths");
+  c->nparams = off;
+  c->used.assign(off, 1);
+  if (g.mode == DBSDE_MODE_NAIS_NET) {
+    // input_layers[K] occupies the tail of the flat vector
+    const long long tail = (long long)L[n - 2] * L[0] + L[n - 2];
+    std::fill(c->used.end() - tail, c->used.end(), 0);
+  }
+  // padded geometry
+  c->Dp = pad16(c->D + 2);
+  if (c->Dp > 128) return fail(c, DBSDE_EINVAL, "D > 126 is not supported by this build (Z epilogue tile)");
+  c->Wp.resize(c->K + 1);
+  c->col.resize(c->K + 1);
+  c->Stot = 0;
+  c->Wmax = 0;
+  for (int j = 0; j <= c->K; ++j) {
+    c->Wp[j] = padw(L[j + 1]);
+    c->col[j] = c->Stot;
+    c->Stot += c->Wp[j];
+    c->Wmax = std::max(c->Wmax, c->Wp[j]);
+  }
+  c->Stot_x = c->has_v ? c->Stot : c->Wp[0];
+  return DBSDE_OK;
+}
+
+PackDesc mk_desc(const float* src, int src_ld, float* dst, int dst_ld, int rows, int cols, int transpose,
+                 int mode, float scale = 1.f) {
+  PackDesc d{};
+  d.src = src;
+  d.src_ld = src_ld;
+  d.dst = dst;
+  d.dst_ld = dst_ld;
+  d.rows = rows;
+  d.cols = cols;
+  d.transpose = transpose;
+  d.mode = mode;
+  d.scale = scale;
+  return d;
+}
+
+// Pack descriptors use "relative" pointers: a src/dst value < 2^40 with bit
+// flags is awkward, so instead we encode param/grad-relative addresses as
+// offsets from a null base and fix them up per call (see fixup_descs).
+constexpr uintptr_t kParamTag = (uintptr_t)1 << 62;
+constexpr uintptr_t kGradTag = (uintptr_t)1 << 61;
+inline float* ptag(long long off) { return (float*)(kParamTag | (uintptr_t)(off * 4)); }
+inline float* gtag(long long off) { return (float*)(kGradTag | (uintptr_t)(off * 4)); }
+
+int build_buffers(dbsde_ctx* c) {
+  const int K = c->K, D = c->D, Dp = c->Dp;
+  int rc;
+  if ((rc = dalloc_t(c, &c->BtIn, (size_t)c->Stot_x * Dp))) return rc;
+  if ((rc = dalloc_t(c, &c->BtZ, (size_t)Dp * c->Stot_x))) return rc;
+  if ((rc = dalloc_t(c, &c->wout, (size_t)c->Wp[K]))) return rc;
+  if ((rc = dalloc_t(c, &c->bout, 16))) return rc;
+  c->Bf.assign(K + 1, nullptr);
+  c->Bb.assign(K + 1, nullptr);
+  c->beta.assign(K + 1, nullptr);
+  c->rtr.assign(K + 1, nullptr);
+  c->abar.assign(K + 1, nullptr);
+  for (int j = 1; j <= K; ++j) {
+    if ((rc = dalloc_t(c, &c->Bf[j], (size_t)c->Wp[j] * c->Wp[j - 1]))) return rc;
+    if ((rc = dalloc_t(c, &c->Bb[j], (size_t)c->Wp[j - 1] * c->Wp[j]))) return rc;
+    if ((rc = dalloc_t(c, &c->beta[j], (size_t)c->Wp[j]))) return rc;
+  }
+  const int LW = c->L[1];
+  if (c->proj) {
+    if ((rc = dalloc_t(c, &c->norms, (size_t)K + 1))) return rc;
+    std::vector<float*> hr(K), ha(K);
+    std::vector<long long> hw(K);
+    for (int j = 1; j <= K; ++j) {
+      if ((rc = dalloc_t(c, &c->rtr[j], (size_t)LW * LW))) return rc;
+      if ((rc = dalloc_t(c, &c->abar[j], (size_t)LW * LW))) return rc;
+      hr[j - 1] = c->rtr[j];
+      ha[j - 1] = c->abar[j];
+      hw[j - 1] = c->B[j - 1].w;
+    }
+    if ((rc = dalloc_t(c, &c->d_rtr, K))) return rc;
+    if ((rc = dalloc_t(c, &c->d_abar, K))) return rc;
+    if ((rc = dalloc_t(c, &c->d_woffs, K))) return rc;
+    HIPC(c, hipMemcpy(c->d_rtr, hr.data(), K * sizeof(float*), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->d_abar, ha.data(), K * sizeof(float*), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->d_woffs, hw.data(), K * sizeof(long long), hipMemcpyHostToDevice));
+  }
+  if ((rc = dalloc_t(c, &c->d_used, (size_t)c->nparams))) return rc;
+  HIPC(c, hipMemcpy(c->d_used, c->used.data(), c->nparams, hipMemcpyHostToDevice));
+  c->opt_nparts = 256;
+  if ((rc = dalloc_t(c, &c->opt_part, c->opt_nparts))) return rc;
+
+  // ---- prep descriptors: flat params -> packed weight buffers
+  std::vector<PackDesc> P;
+  auto add_x_level = [&](int j, const Lin& w, const Lin* b2) {
+    float* dst = c->BtIn + (size_t)c->col[j] * Dp;
+    P.push_back(mk_desc(ptag(w.w), D + 1, dst, Dp, w.out, D + 1, 0, PK_COPY));
+    if (b2) {
+      PackDesc d = mk_desc(ptag(w.b), 1, dst + D + 1, Dp, w.out, 1, 0, PK_ADD2);
+      d.src2 = ptag(b2->b);
+      d.src2_ld = 1;
+      P.push_back(d);
+    } else {
+      P.push_back(mk_desc(ptag(w.b), 1, dst + D + 1, Dp, w.out, 1, 0, PK_COPY));
+    }
+    P.push_back(mk_desc(ptag(w.w), D + 1, c->BtZ + c->col[j], c->Stot_x, w.out, D + 1, 1, PK_COPY));
+  };
+  add_x_level(0, c->in, nullptr);
+  if (c->has_v)
+    for (int j = 1; j <= K; ++j) add_x_level(j, c->V[j - 1], &c->B[j - 1]);
+  for (int j = 1; j <= K; ++j) {
+    const Lin& b = c->B[j - 1];
+    if (c->proj) {
+      PackDesc d = mk_desc(c->rtr[j], LW, c->Bf[j], c->Wp[j - 1], LW, LW, 0, PK_NEGPROJ);
+      d.proj = c->norms + (j - 1);
+      P.push_back(d);
+      d = mk_desc(c->rtr[j], LW, c->Bb[j], c->Wp[j], LW, LW, 1, PK_NEGPROJ);
+      d.proj = c->norms + (j - 1);
+      P.push_back(d);
+    } else {
+      P.push_back(mk_desc(ptag(b.w), b.in, c->Bf[j], c->Wp[j - 1], b.out, b.in, 0, PK_COPY));
+      P.push_back(mk_desc(ptag(b.w), b.in, c->Bb[j], c->Wp[j], b.out, b.in, 1, PK_COPY));
+      P.push_back(mk_desc(ptag(b.b), 1, c->beta[j], 1, b.out, 1, 0, PK_COPY));
+    }
+  }
+  P.push_back(mk_desc(ptag(c->out.w), 1, c->wout, 1, c->out.in, 1, 0, PK_COPY));
+  P.push_back(mk_desc(ptag(c->out.b), 1, c->bout, 1, 1, 1, 0, PK_COPY));
+  c->n_prep = (int)P.size();
+
+  // ---- gradient slabs and finalize descriptors
+  c->slab.assign(K + 1, nullptr);
+  c->slab_mt.assign(K + 1, 0);
+  c->slab_nt.assign(K + 1, 0);
+  auto mkslab = [&](int j, int m, int n) -> int {
+    c->slab_mt[j] = (m + 63) / 64;
+    c->slab_nt[j] = (n + 63) / 64;
+    return dalloc_t(c, &c->slab[j], (size_t)TN_SPLITS * c->slab_mt[j] * 64 * c->slab_nt[j] * 64);
+  };
+  if ((rc = mkslab(0, c->Stot_x, Dp))) return rc;
+  for (int j = 1; j <= K; ++j)
+    if ((rc = mkslab(j, c->Wp[j], c->Wp[j - 1] + (c->has_v ? 0 : 1)))) return rc;
+  c->out_ld = c->L[c->K + 1] + 1;
+  if ((rc = dalloc_t(c, &c->out_slab, (size_t)OUT_SPLITS * c->out_ld))) return rc;
+
+  std::vector<PackDesc> F;
+  auto slabsum = [&](int j, int r0, int c0, int rows, int cols, float* dst, int dst_ld, float scale) {
+    const int ld = c->slab_nt[j] * 64;
+    PackDesc d = mk_desc(c->slab[j] + (size_t)r0 * ld + c0, ld, dst, dst_ld, rows, cols, 0, PK_SLABSUM, scale);
+    d.nslab = TN_SPLITS;
+    d.slab_stride = (long long)c->slab_mt[j] * 64 * ld;
+    F.push_back(d);
+  };
+  slabsum(0, 0, 0, c->in.out, D + 1, gtag(c->in.w), D + 1, 1.f);
+  slabsum(0, 0, D + 1, c->in.out, 1, gtag(c->in.b), 1, 1.f);
+  if (c->has_v)
+    for (int j = 1; j <= K; ++j) {
+      const Lin& v = c->V[j - 1];
+      slabsum(0, c->col[j], 0, v.out, D + 1, gtag(v.w), D + 1, 1.f);
+      slabsum(0, c->col[j], D + 1, v.out, 1, gtag(v.b), 1, 1.f);
+      slabsum(0, c->col[j], D + 1, v.out, 1, gtag(c->B[j - 1].b), 1, 1.f);
+    }
+  for (int j = 1; j <= K; ++j) {
+    const Lin& b = c->B[j - 1];
+    if (c->proj) {
+      slabsum(j, 0, 0, b.out, b.in, c->abar[j], LW, -1.f);  // Abar = -Bbar
+    } else {
+      slabsum(j, 0, 0, b.out, b.in, gtag(b.w), b.in, 1.f);
+      slabsum(j, 0, c->Wp[j - 1], b.out, 1, gtag(b.b), 1, 1.f);
+    }
+  }
+  {
+    PackDesc d = mk_desc(c->out_slab, c->out_ld, gtag(c->out.w), 1, 1, c->L[c->K + 1], 0, PK_SLABSUM);
+    d.nslab = OUT_SPLITS;
+    d.slab_stride = c->out_ld;
+    F.push_back(d);
+    d = mk_desc(c->out_slab + c->L[c->K + 1], c->out_ld, gtag(c->out.b), 1, 1, 1, 0, PK_SLABSUM);
+    d.nslab = OUT_SPLITS;
+    d.slab_stride = c->out_ld;
+    F.push_back(d);
+  }
+  c->n_fin = (int)F.size();
+  if ((rc = dalloc_t(c, &c->d_prep, P.size()))) return rc;
+  if ((rc = dalloc_t(c, &c->d_fin, F.size()))) return rc;
+  // descriptors are stored with tagged pointers; the kernel arguments carry the
+  // real params/grad bases (pack_kernel_tagged below).
+  HIPC(c, hipMemcpy(c->d_prep, P.data(), P.size() * sizeof(PackDesc), hipMemcpyHostToDevice));
+  HIPC(c, hipMemcpy(c->d_fin, F.data(), F.size() * sizeof(PackDesc), hipMemcpyHostToDevice));
+  return DBSDE_OK;
+}
+
+int ensure_rows(dbsde_ctx* c, int Rp, int N) {
+  if (Rp <= c->cap_rows && N <= c->cap_n) return DBSDE_OK;
+  const int nr = std::max(Rp, c->cap_rows), nn = std::max(N, c->cap_n);
+  if (!c->row_allocs.empty()) {
+    HIPC(c, hipStreamSynchronize(c->stream));
+    for (void* p : c->row_allocs) {
+      (void)hipFree(p);
+      c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), p));
+    }
+    c->row_allocs.clear();
+  }
+  const size_t first = c->allocs.size();
+  const size_t R = nr;
+  int rc;
+  const int ldx = c->Dp, S = c->Stot;
+  if ((rc = dalloc_t(c, &c->xin, R * ldx))) return rc;
+  if ((rc = dalloc_t(c, &c->sdw, R * ldx))) return rc;
+  if ((rc = dalloc_t(c, &c->zbar, R * ldx))) return rc;
+  if ((rc = dalloc_t(c, &c->zfull, R * ldx))) return rc;
+  if ((rc = dalloc_t(c, &c->Abuf, R * S))) return rc;
+  if ((rc = dalloc_t(c, &c->Adot, R * S))) return rc;
+  if ((rc = dalloc_t(c, &c->Delta, R * S))) return rc;
+  if ((rc = dalloc_t(c, &c->Alpha, R * S))) return rc;
+  if ((rc = dalloc_t(c, &c->H, R * S))) return rc;
+  if ((rc = dalloc_t(c, &c->Hdot, R * S))) return rc;
+  if ((rc = dalloc_t(c, &c->G, R * S))) return rc;
+  if ((rc = dalloc_t(c, &c->Pbuf[0], R * c->Wmax))) return rc;
+  if ((rc = dalloc_t(c, &c->Pbuf[1], R * c->Wmax))) return rc;
+  if ((rc = dalloc_t(c, &c->u, R + 64))) return rc;
+  if ((rc = dalloc_t(c, &c->rres, R))) return rc;
+  if ((rc = dalloc_t(c, &c->lossrow, R))) return rc;
+  if ((rc = dalloc_t(c, &c->ubar, R))) return rc;
+  if ((rc = dalloc_t(c, &c->loss_part, R / 256 + 2))) return rc;
+  if ((rc = dalloc_t(c, &c->loss_tmp, 16))) return rc;
+  if ((rc = dalloc_t(c, &c->q3S, (size_t)nn + 1))) return rc;
+  c->row_allocs.assign(c->allocs.begin() + first, c->allocs.end());
+  c->cap_rows = nr;
+  c->cap_n = nn;
+  return DBSDE_OK;
+}
+
+// ---------------------------------------------------------------------------
+// chain GEMM dispatch
+// ---------------------------------------------------------------------------
+template <int EPI>
+int chain(dbsde_ctx* c, const char* name, ChainArgs& a, int Rp, int NP, int NT, double flops, double bytes) {
+  dim3 grid(Rp / CH_BM, NP / (16 * NT));
+  if (NP % (16 * NT) != 0) return fail(c, DBSDE_EINVAL, "internal: column tiling mismatch");
+  if (a.K % CH_KC != 0) return fail(c, DBSDE_EINVAL, "internal: K not a multiple of 16");
+  hipStream_t s = c->stream;
+#define CASE_NT(X) \
+  case X:          \
+    RUN(c, name, flops, bytes, chain_gemm_kernel<X, EPI><<<grid, 256, 0, s>>>(a)); \
+    break;
+  switch (NT) {
+    CASE_NT(1)
+    CASE_NT(2)
+    CASE_NT(3)
+    CASE_NT(4)
+    CASE_NT(5)
+    CASE_NT(6)
+    CASE_NT(7)
+    CASE_NT(8)
+    default:
+      return fail(c, DBSDE_EINVAL, "internal: bad NT");
+  }
+#undef CASE_NT
+  return DBSDE_OK;
+}
+
+ChainArgs base_args(dbsde_ctx* c) {
+  ChainArgs a;
+  memset(&a, 0, sizeof(a));
+  a.rho = c->rho;
+  a.act = c->act;
+  return a;
+}
+
+int prep_weights(dbsde_ctx* c, const float* params);
+int finalize_grads(dbsde_ctx* c, const float* params, float* grad);
+
+}  // namespace
+
+// tagged-pointer fixup happens inside a thin wrapper kernel
+namespace dbsde {
+__device__ __forceinline__ const float* untag(const float* p, const float* params, const float* grad) {
+  uintptr_t v = (uintptr_t)p;
+  if (v & ((uintptr_t)1 << 62)) return params + ((v & (((uintptr_t)1 << 61) - 1)) >> 2);
+  if (v & ((uintptr_t)1 << 61)) return grad + ((v & (((uintptr_t)1 << 61) - 1)) >> 2);
+  return p;
+}
+__global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs, const float* params, float* grad) {
+  PackDesc d = descs[blockIdx.y];
+  d.src = untag(d.src, params, grad);
+  d.src2 = untag(d.src2, params, grad);
+  d.dst = (float*)untag(d.dst, params, grad);
+  const int total = d.rows * d.cols;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int r = i / d.cols, cc = i - r * d.cols;
+    float v;
+    if (d.mode == PK_COPY) {
+      v = d.scale * d.src[(size_t)r * d.src_ld + cc];
+    } else if (d.mode == PK_ADD2) {
+      v = d.src[(size_t)r * d.src_ld + cc] + d.src2[(size_t)r * d.src2_ld + cc];
+    } else if (d.mode == PK_NEGPROJ) {
+      const float rv = d.src[(size_t)r * d.src_ld + cc];
+      const float nrm = (float)d.proj[0];
+      float a = rv;
+      if (nrm > 0.98f) a = ((float)0.98994949366116658 * rv) / sqrtf(nrm);
+      a = a + (r == cc ? 0.01f : 0.f);
+      v = -a;
+    } else {
+      double s = 0.0;
+      for (int k = 0; k < d.nslab; ++k) s += d.src[k * d.slab_stride + (size_t)r * d.src_ld + cc];
+      v = d.scale * (float)s;
+    }
+    if (d.transpose)
+      d.dst[(size_t)cc * d.dst_ld + r] = v;
+    else
+      d.dst[(size_t)r * d.dst_ld + cc] = v;
+  }
+}
+__global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, const long long* woffs, int L,
+                                                         float* const* rtr, int ldr, double* norms) {
+  const int j = blockIdx.x;
+  const float* W = params + woffs[j];
+  float* R = rtr[j];
+  __shared__ double red[256];
+  double sq = 0.0;
+  for (int i = threadIdx.x; i < L * L; i += 256) {
+    const int a = i / L, b = i - a * L;
+    float s = 0.f;
+    for (int k = 0; k < L; ++k) s += W[k * L + a] * W[k * L + b];
+    R[a * ldr + b] = s;
+    sq += (double)s * (double)s;
+  }
+  red[threadIdx.x] = sq;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) norms[j] = sqrt(red[0]);
+}
+// Q4 adjoint; W from params, Wbar into grad.
+__global__ void __launch_bounds__(256) proj_adjoint_params_kernel(const float* params, const long long* woffs,
+                                                                  float* const* rtr, float* const* abar,
+                                                                  const double* norms, int L, float* grad) {
+  const int j = blockIdx.y;
+  const float* W = params + woffs[j];
+  const float* R = rtr[j];
+  const float* Ab = abar[j];
+  __shared__ double red[256];
+  double dot = 0.0;
+  for (int i = threadIdx.x; i < L * L; i += 256) dot += (double)Ab[i] * (double)R[i];
+  red[threadIdx.x] = dot;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  dot = red[0];
+  const double n = norms[j];
+  const bool taken = (float)n > 0.98f;
+  const float cA = taken ? (float)(0.98994949366116658 / sqrt(n)) : 1.f;
+  const float cR = taken ? (float)(0.98994949366116658 / sqrt(n) * 0.5 * dot / (n * n)) : 0.f;
+  float* Wb = grad + woffs[j];
+  const int rows0 = blockIdx.x * 8;
+  for (int i = threadIdx.x; i < 8 * L; i += 256) {
+    const int a = rows0 + i / L, b = i % L;
+    if (a >= L) continue;
+    float s = 0.f;
+    for (int k = 0; k < L; ++k) {
+      const float Sv = cA * (Ab[k * L + b] + Ab[b * L + k]) - cR * (R[k * L + b] + R[b * L + k]);
+      s += W[a * L + k] * Sv;
+    }
+    Wb[a * L + b] = s;
+  }
+}
+}  // namespace dbsde
+
+namespace {
+
+int prep_weights(dbsde_ctx* c, const float* params) {
+  hipStream_t s = c->stream;
+  const int LW = c->L[1];
+  if (c->proj) {
+    const double fl = 2.0 * c->K * LW * (double)LW * LW;
+    RUN(c, "rtr", fl, 0.0, rtr_params_kernel<<<c->K, 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, LW, c->norms));
+  }
+  RUN(c, "pack_weights", 0.0, 0.0, pack_tagged_kernel<<<dim3(8, c->n_prep), 256, 0, s>>>(c->d_prep, params, nullptr));
+  return DBSDE_OK;
+}
+
+int finalize_grads(dbsde_ctx* c, const float* params, float* grad) {
+  hipStream_t s = c->stream;
+  RUN(c, "grad_finalize", 0.0, 0.0, pack_tagged_kernel<<<dim3(16, c->n_fin), 256, 0, s>>>(c->d_fin, params, grad));
+  if (c->proj) {
+    const int LW = c->L[1];
+    const double fl = 2.0 * c->K * LW * (double)LW * LW;
+    RUN(c, "proj_adjoint", fl, 0.0,
+        proj_adjoint_params_kernel<<<dim3((LW + 7) / 8, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_rtr, c->d_abar,
+                                                                            c->norms, LW, grad));
+  }
+  return DBSDE_OK;
+}
+
+// forward + input gradient for rows already in xin; leaves u, Abuf, H, Delta, G.
+int forward_and_inputgrad(dbsde_ctx* c, int R, int Rp, bool need_u_only_and_z_store) {
+  (void)need_u_only_and_z_store;
+  const int K = c->K, S = c->Stot, D = c->D;
+  const auto& L = c->L;
+  // x-stack GEMM (a_0 and, for NAIS, the x V_j^T + beta_j parts of every level)
+  {
+    ChainArgs a = base_args(c);
+    a.A = c->xin;
+    a.lda = c->Dp;
+    a.Bt = c->BtIn;
+    a.ldb = c->Dp;
+    a.K = c->Dp;
+    a.out[0] = c->Abuf;
+    a.ldo[0] = S;
+    a.out[1] = c->H;
+    a.ldo[1] = S;
+    a.lvl0_cols = c->Wp[0];
+    int nv = 0;
+    for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
+    const double fl = 2.0 * R * (D + 1) * nv;
+    int rc = chain<EPI_FWD0>(c, "gemm_xstack_fwd", a, Rp, c->Stot_x, nt_for(c->Wp[0]), fl,
+                             4.0 * R * ((D + 1) + nv + L[1]));
+    if (rc) return rc;
+  }
+  for (int j = 1; j <= K; ++j) {
+    ChainArgs a = base_args(c);
+    a.A = c->H + c->col[j - 1];
+    a.lda = S;
+    a.Bt = c->Bf[j];
+    a.ldb = c->Wp[j - 1];
+    a.K = c->Wp[j - 1];
+    a.in[0] = c->has_v ? c->Abuf + c->col[j] : nullptr;
+    a.ldi[0] = S;
+    a.vec[0] = c->beta[j];
+    a.in[1] = c->H + c->col[j - 1];
+    a.ldi[1] = S;
+    a.out[0] = c->Abuf + c->col[j];
+    a.ldo[0] = S;
+    a.out[1] = c->H + c->col[j];
+    a.ldo[1] = S;
+    a.last = j == K;
+    a.out[2] = c->Delta + c->col[K];
+    a.ldo[2] = S;
+    a.vec[1] = c->wout;
+    const double fl = 2.0 * R * L[j] * L[j + 1];
+    int rc = chain<EPI_FWD>(c, "gemm_block_fwd", a, Rp, c->Wp[j], nt_for(c->Wp[j]), fl,
+                            4.0 * R * (L[j] + 4.0 * L[j + 1]));
+    if (rc) return rc;
+  }
+  RUN(c, "rowdot_u", 2.0 * R * L[K + 1], 4.0 * R * L[K + 1],
+      rowdot_kernel<<<Rp / 16, 256, 0, c->stream>>>(c->H + c->col[K], S, c->Wp[K], c->wout, c->bout, c->u, Rp));
+  for (int j = K; j >= 1; --j) {
+    ChainArgs a = base_args(c);
+    a.A = c->Delta + c->col[j];
+    a.lda = S;
+    a.Bt = c->Bb[j];
+    a.ldb = c->Wp[j];
+    a.K = c->Wp[j];
+    a.in[0] = j == K ? nullptr : c->G + c->col[j];
+    a.ldi[0] = S;
+    a.vec[0] = c->wout;
+    a.in[1] = c->Abuf + c->col[j - 1];
+    a.ldi[1] = S;
+    a.out[0] = c->G + c->col[j - 1];
+    a.ldo[0] = S;
+    a.out[1] = c->Delta + c->col[j - 1];
+    a.ldo[1] = S;
+    const double fl = 2.0 * R * L[j] * L[j + 1];
+    int rc = chain<EPI_BWD>(c, "gemm_block_inputgrad", a, Rp, c->Wp[j - 1], nt_for(c->Wp[j - 1]), fl,
+                            4.0 * R * (L[j + 1] + 4.0 * L[j]));
+    if (rc) return rc;
+  }
+  return DBSDE_OK;
+}
+
+int zgemm_args(dbsde_ctx* c, ChainArgs& a) {
+  a.A = c->Delta;
+  a.lda = c->Stot;
+  a.Bt = c->BtZ;
+  a.ldb = c->Stot_x;
+  a.K = c->Stot_x;
+  a.out[0] = c->zfull;
+  a.ldo[0] = c->Dp;
+  return DBSDE_OK;
+}
+
+double zgemm_flops(dbsde_ctx* c, int R) {
+  int nv = 0;
+  for (int j = 0; j <= (c->has_v ? c->K : 0); ++j) nv += c->L[j + 1];
+  return 2.0 * R * nv * c->D;
+}
+
+int validate_batch(dbsde_ctx* c, const dbsde_batch* b) {
+  if (!b) return fail(c, DBSDE_EINVAL, "batch is NULL");
+  if (b->M < 1 || b->N < 1) return fail(c, DBSDE_EINVAL, "M and N must be >= 1");
+  if ((long long)b->M * (b->N + 1) > (1LL << 30)) return fail(c, DBSDE_EINVAL, "M*(N+1) too large");
+  if (!b->Xi) return fail(c, DBSDE_EINVAL, "Xi is NULL");
+  if (b->xi_rows != 1 && b->xi_rows != b->M) return fail(c, DBSDE_EINVAL, "Xi must have 1 or M rows");
+  if (b->W && !b->t) return fail(c, DBSDE_EINVAL, "t is required with W");
+  return DBSDE_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int dbsde_abi_version(void) { return DBSDE_ABI_VERSION; }
+
+const char* dbsde_last_error(const dbsde_ctx* ctx) {
+  if (ctx && !ctx->err.empty()) return ctx->err.c_str();
+  return g_last_error.c_str();
+}
+
+int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
+  if (!cfg || !out) return fail(nullptr, DBSDE_EINVAL, "cfg/out is NULL");
+  *out = nullptr;
+  dbsde_ctx* c = new dbsde_ctx();
+  c->cfg = *cfg;
+  c->device = cfg->device;
+  int rc = build_net(c);
+  if (!rc) {
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) rc = fail(c, DBSDE_EHIP, "no HIP device available");
+    else if (cfg->device < 0 || cfg->device >= ndev) rc = fail(c, DBSDE_EINVAL, "bad device ordinal");
+    else if ((e = hipSetDevice(cfg->device)) != hipSuccess) rc = fail(c, DBSDE_EHIP, hipGetErrorString(e));
+  }
+  if (!rc) rc = build_buffers(c);
+  if (rc) {
+    g_last_error = c->err;
+    dbsde_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return DBSDE_OK;
+}
+
+void dbsde_destroy(dbsde_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& r : c->pending) {
+    c->ev_pool.push_back(r.e0);
+    c->ev_pool.push_back(r.e1);
+  }
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  for (void* p : c->allocs) (void)hipFree(p);
+  delete c;
+}
+
+int dbsde_set_stream(dbsde_ctx* c, void* s) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  c->stream = (hipStream_t)s;
+  return DBSDE_OK;
+}
+
+long long dbsde_param_count(const dbsde_ctx* c) { return c ? c->nparams : -1; }
+
+int dbsde_param_used_mask(const dbsde_ctx* c, unsigned char* mask, long long n) {
+  if (!c || !mask || n != c->nparams) return fail(nullptr, DBSDE_EINVAL, "bad mask buffer");
+  memcpy(mask, c->used.data(), (size_t)n);
+  return DBSDE_OK;
+}
+
+int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, float* grad,
+                    const dbsde_outputs* out) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!params) return fail(c, DBSDE_EINVAL, "params is NULL");
+  int rc = validate_batch(c, b);
+  if (rc) return rc;
+  HIPC(c, hipSetDevice(c->device));
+  const int M = b->M, N = b->N, N1 = N + 1, D = c->D, K = c->K, S = c->Stot;
+  const int R = M * N1, Rp = (R + CH_BM - 1) / CH_BM * CH_BM;
+  if ((rc = ensure_rows(c, Rp, N))) return rc;
+  hipStream_t s = c->stream;
+  const auto& L = c->L;
+  const dbsde_problem& pr = c->cfg.problem;
+
+  if ((rc = prep_weights(c, params))) return rc;
+
+  // ---- rollout (network-independent: mu/sigma never read Y, Z)
+  if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
+  {
+    RolloutArgs ra{};
+    ra.M = M;
+    ra.N = N;
+    ra.D = D;
+    ra.ldx = c->Dp;
+    ra.t = b->t;
+    ra.W = b->W;
+    ra.Xi = b->Xi;
+    ra.xi_rows = b->xi_rows;
+    ra.T = c->cfg.T;
+    ra.seed = b->seed;
+    ra.offset = b->offset;
+    ra.path0 = b->path0;
+    ra.mu_a = pr.mu_a;
+    ra.sig_a = pr.sig_a;
+    ra.sig_b = pr.sig_b;
+    ra.xin = c->xin;
+    ra.sdw = c->sdw;
+    const int nthr = M * D;
+    RUN(c, "rollout", 6.0 * (double)M * N * D, 4.0 * (double)M * N * D * (b->W ? 4 : 3),
+        rollout_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
+  }
+  const bool q3 = pr.q3 && D == 1;
+  if (q3) RUN(c, "q3_sum", 0.0, 4.0 * M * N, q3_sum_kernel<<<N, 256, 0, s>>>(c->sdw, c->Dp, M, N, c->q3S));
+
+  if ((rc = forward_and_inputgrad(c, R, Rp, false))) return rc;
+
+  // ---- Z GEMM + residuals / cotangents / loss rows
+  {
+    ChainArgs a = base_args(c);
+    zgemm_args(c, a);
+    a.R = R;
+    a.N1 = N1;
+    a.D = D;
+    a.xin = c->xin;
+    a.sdw = c->sdw;
+    a.ldx = c->Dp;
+    a.u = c->u;
+    a.q3S = q3 ? c->q3S : nullptr;
+    a.phi_r = pr.phi_r;
+    a.phi_c = pr.phi_c;
+    a.phi_zz = pr.phi_zz;
+    a.strike = pr.strike;
+    a.g_kind = pr.g_kind;
+    a.zbar = c->zbar;
+    a.rres = c->rres;
+    a.lossrow = c->lossrow;
+    if ((rc = chain<EPI_COTAN>(c, "gemm_z_cotangent", a, Rp, c->Dp, c->Dp / 16, zgemm_flops(c, R),
+                               4.0 * R * (c->Stot_x + 5.0 * D))))
+      return rc;
+  }
+  RUN(c, "ubar_loss", 0.0, 16.0 * R,
+      ubar_kernel<<<Rp / 256 + 1, 256, 0, s>>>(c->rres, c->xin, c->Dp, R, Rp, N1, pr.phi_r, c->lossrow, c->ubar,
+                                               c->loss_part));
+  float* loss_dst = (out && out->loss) ? out->loss : c->loss_tmp;
+  RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, s>>>(c->loss_part, Rp / 256 + 1, loss_dst));
+
+  if (grad) {
+    // ---- forward tangent along zbar
+    {
+      ChainArgs a = base_args(c);
+      a.A = c->zbar;
+      a.lda = c->Dp;
+      a.Bt = c->BtIn;
+      a.ldb = c->Dp;
+      a.K = c->Dp;
+      a.in[0] = c->Abuf;
+      a.ldi[0] = S;
+      a.out[0] = c->Adot;
+      a.ldo[0] = S;
+      a.out[1] = c->Hdot;
+      a.ldo[1] = S;
+      a.lvl0_cols = c->Wp[0];
+      int nv = 0;
+      for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
+      if ((rc = chain<EPI_TAN0>(c, "gemm_xstack_tangent", a, Rp, c->Stot_x, nt_for(c->Wp[0]),
+                                2.0 * R * D * nv, 4.0 * R * (D + 2.0 * nv + L[1]))))
+        return rc;
+    }
+    for (int j = 1; j <= K; ++j) {
+      ChainArgs a = base_args(c);
+      a.A = c->Hdot + c->col[j - 1];
+      a.lda = S;
+      a.Bt = c->Bf[j];
+      a.ldb = c->Wp[j - 1];
+      a.K = c->Wp[j - 1];
+      a.in[0] = c->has_v ? c->Adot + c->col[j] : nullptr;
+      a.ldi[0] = S;
+      a.in[1] = c->Hdot + c->col[j - 1];
+      a.ldi[1] = S;
+      a.in[2] = c->Abuf + c->col[j];
+      a.ldi[2] = S;
+      a.out[0] = c->Adot + c->col[j];
+      a.ldo[0] = S;
+      a.out[1] = c->Hdot + c->col[j];
+      a.ldo[1] = S;
+      a.last = j == K;
+      a.out[2] = c->Alpha + c->col[K];
+      a.ldo[2] = S;
+      a.vec[0] = c->wout;
+      a.ubar = c->ubar;
+      if ((rc = chain<EPI_TAN>(c, "gemm_block_tangent", a, Rp, c->Wp[j], nt_for(c->Wp[j]),
+                               2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j] + 6.0 * L[j + 1]))))
+        return rc;
+    }
+    // ---- reverse over (primal, tangent)
+    for (int j = K; j >= 1; --j) {
+      ChainArgs a = base_args(c);
+      a.A = c->Alpha + c->col[j];
+      a.lda = S;
+      a.Bt = c->Bb[j];
+      a.ldb = c->Wp[j];
+      a.K = c->Wp[j];
+      a.in[0] = j == K ? nullptr : c->Pbuf[(j + 1) & 1];
+      a.ldi[0] = c->Wmax;
+      a.ubar = c->ubar;
+      a.vec[0] = c->wout;
+      a.in[1] = c->Abuf + c->col[j - 1];
+      a.ldi[1] = S;
+      a.in[2] = c->G + c->col[j - 1];
+      a.ldi[2] = S;
+      a.in[3] = c->Adot + c->col[j - 1];
+      a.ldi[3] = S;
+      a.out[0] = c->Pbuf[j & 1];
+      a.ldo[0] = c->Wmax;
+      a.out[1] = c->Alpha + c->col[j - 1];
+      a.ldo[1] = S;
+      if ((rc = chain<EPI_REV>(c, "gemm_block_reverse", a, Rp, c->Wp[j - 1], nt_for(c->Wp[j - 1]),
+                               2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j + 1] + 6.0 * L[j]))))
+        return rc;
+    }
+    // ---- parameter gradients
+    HIPC(c, hipMemsetAsync(grad, 0, (size_t)c->nparams * 4, s));
+    TNArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    const int rps = ((Rp + TN_SPLITS - 1) / TN_SPLITS + TN_KC - 1) / TN_KC * TN_KC;
+    ta.rows_per_split = rps;
+    ta.Rp = Rp;
+    double tfl = 0.0;
+    {
+      TNProb& p0 = ta.prob[0];
+      p0.A[0] = c->Alpha;
+      p0.lda[0] = S;
+      p0.nA[0] = c->Stot_x;
+      p0.B[0] = c->xin;
+      p0.ldb[0] = c->Dp;
+      p0.nB[0] = c->Dp;
+      p0.A[1] = c->Delta;
+      p0.lda[1] = S;
+      p0.nA[1] = c->Stot_x;
+      p0.B[1] = c->zbar;
+      p0.ldb[1] = c->Dp;
+      p0.nB[1] = c->Dp;
+      p0.npairs = 2;
+      p0.ones_col = -1;
+      p0.mt = c->slab_mt[0];
+      p0.nt = c->slab_nt[0];
+      p0.slab = c->slab[0];
+      int nv = 0;
+      for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
+      tfl += 2.0 * 2.0 * R * nv * (D + 2);
+    }
+    int maxt = ta.prob[0].mt * ta.prob[0].nt;
+    for (int j = 1; j <= K; ++j) {
+      TNProb& pj = ta.prob[j];
+      pj.A[0] = c->Alpha + c->col[j];
+      pj.lda[0] = S;
+      pj.nA[0] = c->Wp[j];
+      pj.B[0] = c->H + c->col[j - 1];
+      pj.ldb[0] = S;
+      pj.nB[0] = c->Wp[j - 1];
+      pj.A[1] = c->Delta + c->col[j];
+      pj.lda[1] = S;
+      pj.nA[1] = c->Wp[j];
+      pj.B[1] = c->Hdot + c->col[j - 1];
+      pj.ldb[1] = S;
+      pj.nB[1] = c->Wp[j - 1];
+      pj.npairs = 2;
+      pj.ones_col = c->has_v ? -1 : c->Wp[j - 1];
+      pj.mt = c->slab_mt[j];
+      pj.nt = c->slab_nt[j];
+      pj.slab = c->slab[j];
+      maxt = std::max(maxt, pj.mt * pj.nt);
+      tfl += 2.0 * 2.0 * R * L[j] * (L[j + 1] + (c->has_v ? 0 : 1));
+    }
+    if (K + 1 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
+    RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, TN_SPLITS, K + 1), 256, 0, s>>>(ta));
+    const int orps = (Rp + OUT_SPLITS - 1) / OUT_SPLITS;
+    RUN(c, "out_layer_grad", 4.0 * R * L[K + 1], 8.0 * R * L[K + 1],
+        outgrad_kernel<<<OUT_SPLITS, 256, 0, s>>>(c->ubar, c->H + c->col[K], c->Hdot + c->col[K], S, L[K + 1], orps,
+                                                  Rp, c->out_ld, c->out_slab));
+    if ((rc = finalize_grads(c, params, grad))) return rc;
+  }
+
+  if (out && (out->X || out->Y || out->Z)) {
+    const long long n = (long long)R * D;
+    RUN(c, "export", 0.0, 0.0,
+        export_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, out->X,
+                                                                  out->Y, out->Z));
+  }
+  return DBSDE_OK;
+}
+
+int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const float* X, float* u, float* Du) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!params || !t || !X || R < 1) return fail(c, DBSDE_EINVAL, "bad net_u arguments");
+  HIPC(c, hipSetDevice(c->device));
+  const int Rp = (R + CH_BM - 1) / CH_BM * CH_BM, D = c->D;
+  int rc;
+  if ((rc = ensure_rows(c, Rp, 1))) return rc;
+  hipStream_t s = c->stream;
+  if ((rc = prep_weights(c, params))) return rc;
+  const long long n = (long long)Rp * c->Dp;
+  RUN(c, "netu_input", 0.0, 0.0,
+      netu_input_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
+  if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
+  if ((rc = forward_and_inputgrad(c, R, Rp, true))) return rc;
+  {
+    ChainArgs a = base_args(c);
+    zgemm_args(c, a);
+    if ((rc = chain<EPI_STORE>(c, "gemm_z", a, Rp, c->Dp, c->Dp / 16, zgemm_flops(c, R), 0.0))) return rc;
+  }
+  const long long m = (long long)R * D;
+  RUN(c, "export", 0.0, 0.0,
+      export_kernel<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, nullptr, u,
+                                                                Du));
+  return DBSDE_OK;
+}
+
+int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, float* v, const dbsde_optim* o) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!params || !grad || !o) return fail(c, DBSDE_EINVAL, "bad optimizer arguments");
+  if (o->kind < 0 || o->kind > 2) return fail(c, DBSDE_EINVAL, "unknown optimizer kind");
+  if (o->kind != DBSDE_OPT_SGD && (!m || !v)) return fail(c, DBSDE_EINVAL, "Adam needs m and v");
+  if (o->step < 1) return fail(c, DBSDE_EINVAL, "step must be >= 1");
+  HIPC(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const long long n = c->nparams;
+  OptArgs a{};
+  a.kind = o->kind;
+  a.lr = o->lr;
+  a.beta2 = o->beta2;
+  a.eps = o->eps;
+  a.wd = o->weight_decay;
+  a.max_norm = o->max_norm;
+  a.omb1 = (float)(1.0 - (double)o->beta1);
+  a.omb2 = (float)(1.0 - (double)o->beta2);
+  const double bc1 = 1.0 - std::pow((double)o->beta1, (double)o->step);
+  const double bc2 = 1.0 - std::pow((double)o->beta2, (double)o->step);
+  a.step_size = (float)((double)o->lr / bc1);
+  a.bc2_sqrt = (float)std::sqrt(bc2);
+  a.nparts = c->opt_nparts;
+  if (o->max_norm > 0.f)
+    RUN(c, "grad_sqnorm", 2.0 * n, 4.0 * n, sqnorm_kernel<<<c->opt_nparts, 256, 0, s>>>(grad, c->d_used, n, c->opt_part));
+  RUN(c, "optimizer", 10.0 * n, 24.0 * n,
+      optim_kernel<<<256, 256, 0, s>>>(params, grad, m, v, c->d_used, n, c->opt_part, a));
+  return DBSDE_OK;
+}
+
+int dbsde_profile_enable(dbsde_ctx* c, int enable) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  c->prof = enable != 0;
+  return DBSDE_OK;
+}
+
+static int collect(dbsde_ctx* c) {
+  if (c->pending.empty()) return DBSDE_OK;
+  HIPC(c, hipStreamSynchronize(c->stream));
+  for (auto& r : c->pending) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, r.e0, r.e1);
+    ProfAgg& a = c->agg[r.id];
+    a.ms += ms;
+    a.flops += r.flops;
+    a.bytes += r.bytes;
+    a.n += 1;
+    c->ev_pool.push_back(r.e0);
+    c->ev_pool.push_back(r.e1);
+  }
+  c->pending.clear();
+  return DBSDE_OK;
+}
+
+int dbsde_profile_count(dbsde_ctx* c) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  int rc = collect(c);
+  if (rc) return rc;
+  return (int)c->agg.size();
+}
+
+int dbsde_profile_read(dbsde_ctx* c, int idx, char* name, int name_len, double* total_ms, double* flops,
+                       double* bytes, long long* launches) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  int rc = collect(c);
+  if (rc) return rc;
+  if (idx < 0 || idx >= (int)c->agg.size()) return fail(c, DBSDE_EINVAL, "profile index out of range");
+  const ProfAgg& a = c->agg[idx];
+  if (name && name_len > 0) {
+    strncpy(name, a.name.c_str(), name_len - 1);
+    name[name_len - 1] = 0;
+  }
+  if (total_ms) *total_ms = a.ms;
+  if (flops) *flops = a.flops;
+  if (bytes) *bytes = a.bytes;
+  if (launches) *launches = a.n;
+  return DBSDE_OK;
+}
+
+int dbsde_profile_reset(dbsde_ctx* c) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  int rc = collect(c);
+  if (rc) return rc;
+  for (auto& a : c->agg) {
+    a.ms = a.flops = a.bytes = 0;
+    a.n = 0;
+  }
+  return DBSDE_OK;
+}
+
+}  // extern "C"

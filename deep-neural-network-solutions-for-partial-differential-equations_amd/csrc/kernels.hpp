@@ -1,0 +1,731 @@
+// kernels.hpp -- HIP kernels (gfx950 / CDNA4) of the deep-BSDE training step.
+//
+// Row layout: one "row" = one (path m, time n) pair, r = m*(N+1)+n, exactly the
+// reference's X[M, N+1, D] order (DeepBSDE.py:242).  All activation buffers are
+// row-major [Rp, ld] fp32 with Rp a multiple of 64 and ld a multiple of 16.
+// Padding rows/columns are zero and stay zero (every activation has act(0)=0).
+//
+// Unified network (see oracle/timeparallel.py for the derivation):
+//   a_0 = x W_in^T + b_in,  h_1 = act(a_0)
+//   a_j = h_j B_j^T + [x V_j^T] + beta_j,  h_{j+1} = act(a_j) + rho h_j   (j=1..K)
+//   u   = h_{K+1}.w_out + b_out
+// "level j" of an [Rp, Stot] buffer holds the width-L_{j+1} quantity of a_j.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dbsde {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+enum Act { ACT_SINE = 0, ACT_RELU = 1, ACT_TANH = 2 };
+
+__device__ __forceinline__ float act_f(int act, float a) {
+  if (act == ACT_SINE) return sinf(a);
+  if (act == ACT_TANH) return tanhf(a);
+  return a > 0.f ? a : 0.f;
+}
+__device__ __forceinline__ float act_d1(int act, float a) {
+  if (act == ACT_SINE) return cosf(a);
+  if (act == ACT_TANH) {
+    float t = tanhf(a);
+    return 1.f - t * t;
+  }
+  return a > 0.f ? 1.f : 0.f;
+}
+__device__ __forceinline__ void act_d12(int act, float a, float& d1, float& d2) {
+  if (act == ACT_SINE) {
+    float s, c;
+    sincosf(a, &s, &c);
+    d1 = c;
+    d2 = -s;
+  } else if (act == ACT_TANH) {
+    float t = tanhf(a);
+    d1 = 1.f - t * t;
+    d2 = -2.f * t * d1;
+  } else {
+    d1 = a > 0.f ? 1.f : 0.f;
+    d2 = 0.f;
+  }
+}
+
+__device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// --------------------------------------------------------------------------
+// Philox4x32-10 + Box-Muller (device Brownian increments)
+// --------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+__device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned long long offset,
+                                               uint32_t m, uint32_t n, uint32_t d) {
+  uint32_t c[4] = {d, n, m, (uint32_t)offset};
+  philox4x32_10(c, (uint32_t)seed ^ (uint32_t)(offset >> 32), (uint32_t)(seed >> 32));
+  // two uniforms in (0,1] -> one standard normal
+  float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
+
+// --------------------------------------------------------------------------
+// Euler-Maruyama rollout  (DeepBSDE.py:218-222, nd_BSPDE_case.py:258-261)
+// thread per (path m, dim d); sequential over n.  Writes the network input
+// rows xin[r] = [t, X_1..X_D, 1, 0...] and sdw[r] = sigma(X_n) * dW_n.
+// The arithmetic order and rounding is the reference's (no contraction):
+//   X1 = (X0 + (mu_a*X0)*(t1-t0)) + (sig_a*X0 + sig_b)*(W1-W0)
+// --------------------------------------------------------------------------
+struct RolloutArgs {
+  int M, N, D, ldx;
+  const float* t;   // [M, N+1] or null (uniform grid)
+  const float* W;   // [M, N+1, D] or null (Philox)
+  const float* Xi;  // [xi_rows, D]
+  int xi_rows;
+  float T;
+  unsigned long long seed, offset;
+  long long path0;
+  float mu_a, sig_a, sig_b;
+  float* xin;       // [Rp, ldx]
+  float* sdw;       // [Rp, ldx]   (cols 0..D-1)
+};
+
+__global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= p.M * p.D) return;
+  const int m = gid / p.D, d = gid - m * p.D;
+  const int N1 = p.N + 1;
+  float x = p.Xi[(p.xi_rows == 1 ? 0 : m) * p.D + d];
+  const float dtu = p.T / (float)p.N;
+  const float sqdt = sqrtf(dtu);
+  float t0 = p.t ? p.t[(size_t)m * N1] : 0.0f;
+  float w0 = p.W ? p.W[(size_t)m * N1 * p.D + d] : 0.0f;
+  size_t r = (size_t)m * N1;
+  for (int n = 0; n < p.N; ++n, ++r) {
+    float* xr = p.xin + r * p.ldx;
+    xr[1 + d] = x;
+    if (d == 0) {
+      xr[0] = t0;
+      xr[p.D + 1] = 1.0f;
+    }
+    float t1, dw;
+    if (p.W) {
+      t1 = p.t[(size_t)m * N1 + n + 1];
+      float w1 = p.W[((size_t)m * N1 + n + 1) * p.D + d];
+      dw = __fsub_rn(w1, w0);
+      w0 = w1;
+    } else {
+      t1 = p.t ? p.t[(size_t)m * N1 + n + 1] : (float)((double)p.T * (double)(n + 1) / (double)p.N);
+      dw = sqdt * philox_normal(p.seed, p.offset, (uint32_t)(p.path0 + m), (uint32_t)n, (uint32_t)d);
+    }
+    const float dt = __fsub_rn(t1, t0);
+    const float sg = __fadd_rn(__fmul_rn(p.sig_a, x), p.sig_b);
+    const float s = __fmul_rn(sg, dw);
+    p.sdw[r * p.ldx + d] = s;
+    x = __fadd_rn(__fadd_rn(x, __fmul_rn(__fmul_rn(p.mu_a, x), dt)), s);
+    t0 = t1;
+  }
+  float* xr = p.xin + r * p.ldx;  // n = N
+  xr[1 + d] = x;
+  p.sdw[r * p.ldx + d] = 0.0f;
+  if (d == 0) {
+    xr[0] = t0;
+    xr[p.D + 1] = 1.0f;
+  }
+}
+
+// Q3 (D == 1): S_n = sum over paths of sdw[m, n]   (1d_BSPDE_case.py:271-273)
+__global__ void __launch_bounds__(256) q3_sum_kernel(const float* sdw, int ldx, int M, int N, float* S) {
+  const int n = blockIdx.x;
+  __shared__ float red[256];
+  float acc = 0.f;
+  for (int m = threadIdx.x; m < M; m += 256) acc += sdw[((size_t)m * (N + 1) + n) * ldx];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) S[n] = red[0];
+}
+
+// --------------------------------------------------------------------------
+// Chain GEMM:  C[Rp, NP] = A[Rp, K] * Bt[NP, K]^T  with a fused epilogue.
+// fp32 MFMA v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulate).
+// Workgroup: 4 waves, 64 rows x (16*NT) columns; each wave 16 rows x 16*NT.
+// K is staged through LDS in chunks of 16 (double buffered, register staged).
+// Inside a 16-chunk, lane group q=lane>>4 feeds k = 4q+i to MFMA i (the sum
+// over k is order-free), so each lane reads one float4 of A and of Bt.
+// --------------------------------------------------------------------------
+enum Epi {
+  EPI_FWD0 = 0,   // a = acc -> out0 ; level-0 cols: h1 = act(a) -> out1
+  EPI_FWD,        // a = acc + (in0 ? in0 : vec0) ; h = act(a) + rho*in1 ; out0=a, out1=h ; last: out2 = vec1*act'(a)
+  EPI_BWD,        // g = acc + rho*(in0 ? in0 : vec0) ; out0=g ; out1 = g*act'(in1)
+  EPI_COTAN,      // Z GEMM: residuals, zbar, loss rows
+  EPI_TAN0,       // adot = acc -> out0 ; level-0 cols: hdot1 = act'(in0)*adot -> out1
+  EPI_TAN,        // adot = acc + (in0?in0:0); hdot = act'(in2)*adot + rho*in1 ; last: out2 = alpha_K
+  EPI_REV,        // p = acc + rho*(in0 ? in0 : ubar*vec0) ; out0=p ; out1 = p*act'(in1) + in2*in3*act''(in1)
+  EPI_STORE,      // out0 = acc (net_u Z / plain)
+};
+
+struct ChainArgs {
+  const float* A;
+  int lda;
+  const float* Bt;
+  int ldb;
+  int K;
+  const float* in[4];
+  int ldi[4];
+  float* out[3];
+  int ldo[3];
+  const float* vec[2];
+  const float* ubar;
+  float rho;
+  int act;
+  int lvl0_cols;  // EPI_FWD0 / EPI_TAN0: number of padded level-0 columns
+  int last;       // EPI_FWD / EPI_TAN: j == K
+  // --- EPI_COTAN
+  int R, N1, D;
+  const float* xin;   // [Rp, ldx]
+  const float* sdw;   // [Rp, ldx]
+  int ldx;
+  const float* u;     // [Rp]
+  const float* q3S;   // [N] or null
+  float phi_r, phi_c, phi_zz, strike;
+  int g_kind;
+  float* zbar;        // [Rp, ldx]
+  float* rres;        // [Rp]
+  float* lossrow;     // [Rp]
+};
+
+constexpr int CH_BM = 64;
+constexpr int CH_KC = 16;
+constexpr int CH_LS = 20;  // LDS row stride in floats (16 + 4 pad)
+
+template <int NT>
+__device__ __forceinline__ void chain_mainloop(const ChainArgs& p, int row0, int col0, floatx4 (&acc)[NT]) {
+  __shared__ float As[2][CH_BM * CH_LS];
+  __shared__ float Bs[2][16 * NT * CH_LS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NBV = (64 * NT + 255) / 256;  // float4 B loads per thread
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const float* Ag = p.A + (size_t)(row0 + (tid >> 2)) * p.lda + (tid & 3) * 4;
+  floatx4 areg;
+  floatx4 breg[NBV];
+  const int nk = p.K / CH_KC;
+
+  auto gload = [&](int kc) {
+    areg = *(const floatx4*)(Ag + kc * CH_KC);
+#pragma unroll
+    for (int i = 0; i < NBV; ++i) {
+      int idx = tid + i * 256;
+      if (idx < 64 * NT) {
+        int br = idx >> 2, bc = (idx & 3) * 4;
+        breg[i] = *(const floatx4*)(p.Bt + (size_t)(col0 + br) * p.ldb + kc * CH_KC + bc);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    *(floatx4*)&As[buf][(tid >> 2) * CH_LS + (tid & 3) * 4] = areg;
+#pragma unroll
+    for (int i = 0; i < NBV; ++i) {
+      int idx = tid + i * 256;
+      if (idx < 64 * NT) *(floatx4*)&Bs[buf][(idx >> 2) * CH_LS + (idx & 3) * 4] = breg[i];
+    }
+  };
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nk) gload(kc + 1);
+    const floatx4 a = *(const floatx4*)&As[buf][(wave * 16 + (lane & 15)) * CH_LS + (lane >> 4) * 4];
+    floatx4 b[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b[t] = *(const floatx4*)&Bs[buf][(t * 16 + (lane & 15)) * CH_LS + (lane >> 4) * 4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = mfma4(a.x, b[t].x, acc[t]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = mfma4(a.y, b[t].y, acc[t]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = mfma4(a.z, b[t].z, acc[t]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = mfma4(a.w, b[t].w, acc[t]);
+    if (kc + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ float red16(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+template <int NT, int EPI>
+__global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
+  const int row0 = blockIdx.x * CH_BM;
+  const int col0 = blockIdx.y * 16 * NT;
+  floatx4 acc[NT];
+  chain_mainloop<NT>(p, row0, col0, acc);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rbase = row0 + wave * 16 + (lane >> 4) * 4;
+  const int cl = lane & 15;
+
+  if constexpr (EPI == EPI_COTAN) {
+    // Each 16-lane group owns 4 rows; the workgroup tile covers every column
+    // (the engine launches this epilogue with a single column tile).
+    const int D = p.D;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = rbase + j;
+      const bool valid = row < p.R;
+      const int n = valid ? row % p.N1 : 0;
+      const bool term = n == p.N1 - 1;
+      const float* xr = p.xin + (size_t)row * p.ldx;
+      const float* sr = p.sdw + (size_t)row * p.ldx;
+      float s_zs = 0.f, s_xz = 0.f, s_zz = 0.f, s_x = 0.f, s_xx = 0.f, z1 = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int c = col0 + t * 16 + cl;  // Zfull column (0 = t, 1..D = Z)
+        const float z = acc[t][j];
+        if (c >= 1 && c <= D) {
+          const float xv = xr[c];
+          s_zs += z * sr[c - 1];
+          s_xz += xv * z;
+          s_zz += z * z;
+          s_x += xv;
+          s_xx += xv * xv;
+        }
+        if (c == 1) z1 = z;
+      }
+      s_zs = red16(s_zs);
+      s_xz = red16(s_xz);
+      s_zz = red16(s_zz);
+      s_x = red16(s_x);
+      s_xx = red16(s_xx);
+      z1 = red16(z1);
+      float res = 0.f, lossv = 0.f, coefY = 0.f, S = 0.f, dt = 0.f, gsc = 0.f;
+      if (valid) {
+        const float y = p.u[row];
+        if (!term) {
+          dt = xr[p.ldx] - xr[0];
+          // Q3 (D == 1, 1d_BSPDE_case.py:271-273): Z_i * sum_j (sigma dW)_j
+          if (p.q3S) S = p.q3S[n];
+          const float zs = p.q3S ? z1 * S : s_zs;
+          const float phi = p.phi_r * (y - p.phi_c * s_xz) + p.phi_zz * s_zz;
+          const float ytil = y + phi * dt + zs;
+          res = p.u[row + 1] - ytil;
+          lossv = res * res;
+          coefY = -2.f * res;
+        } else {
+          float g;
+          if (p.g_kind == 0) {
+            g = s_xx;
+          } else if (p.g_kind == 1) {
+            const float v = s_x - p.strike;
+            g = v > 0.f ? v : 0.f;
+            gsc = v > 0.f ? 1.f : 0.f;
+          } else if (p.g_kind == 2) {
+            const float v = s_x / (float)D - p.strike;
+            g = v > 0.f ? v : 0.f;
+            gsc = v > 0.f ? 1.f / (float)D : 0.f;
+          } else {
+            const float q = 0.5f + 0.5f * s_xx;
+            g = logf(q);
+            gsc = 1.f / q;
+          }
+          res = y - g;
+          lossv = res * res;
+        }
+      }
+      // zbar row and the terminal |Z - grad g|^2
+      float tz = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int c = col0 + t * 16 + cl;
+        const float z = acc[t][j];
+        float zb = 0.f;
+        if (valid && c >= 1 && c <= D) {
+          const float xv = xr[c];
+          if (!term) {
+            const float dphidz = -p.phi_r * p.phi_c * xv + 2.f * p.phi_zz * z;
+            const float sd = p.q3S ? S : sr[c - 1];
+            zb = coefY * (dphidz * dt + sd);
+          } else {
+            const float dg = (p.g_kind == 0) ? 2.f * xv : (p.g_kind == 3 ? xv * gsc : gsc);
+            const float e = z - dg;
+            tz += e * e;
+            zb = 2.f * e;
+          }
+        }
+        p.zbar[(size_t)row * p.ldx + c] = zb;
+        p.out[0][(size_t)row * p.ldo[0] + c] = z;
+      }
+      tz = red16(tz);
+      if (cl == 0) {
+        p.rres[row] = valid ? res : 0.f;
+        p.lossrow[row] = valid ? lossv + tz : 0.f;
+      }
+    }
+    return;
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int c = col0 + t * 16 + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const size_t row = (size_t)(rbase + j);
+        const float v = acc[t][j];
+        if constexpr (EPI == EPI_STORE) {
+          p.out[0][row * p.ldo[0] + c] = v;
+        } else if constexpr (EPI == EPI_FWD0) {
+          p.out[0][row * p.ldo[0] + c] = v;
+          if (c < p.lvl0_cols) p.out[1][row * p.ldo[1] + c] = act_f(p.act, v);
+        } else if constexpr (EPI == EPI_FWD) {
+          const float a = v + (p.in[0] ? p.in[0][row * p.ldi[0] + c] : p.vec[0][c]);
+          const float h = act_f(p.act, a) + (p.rho != 0.f ? p.rho * p.in[1][row * p.ldi[1] + c] : 0.f);
+          p.out[0][row * p.ldo[0] + c] = a;
+          p.out[1][row * p.ldo[1] + c] = h;
+          if (p.last) p.out[2][row * p.ldo[2] + c] = p.vec[1][c] * act_d1(p.act, a);
+        } else if constexpr (EPI == EPI_BWD) {
+          const float gn = p.rho == 0.f ? 0.f : (p.in[0] ? p.in[0][row * p.ldi[0] + c] : p.vec[0][c]);
+          const float g = v + p.rho * gn;
+          p.out[0][row * p.ldo[0] + c] = g;
+          p.out[1][row * p.ldo[1] + c] = g * act_d1(p.act, p.in[1][row * p.ldi[1] + c]);
+        } else if constexpr (EPI == EPI_TAN0) {
+          p.out[0][row * p.ldo[0] + c] = v;
+          if (c < p.lvl0_cols) p.out[1][row * p.ldo[1] + c] = act_d1(p.act, p.in[0][row * p.ldi[0] + c]) * v;
+        } else if constexpr (EPI == EPI_TAN) {
+          const float ad = v + (p.in[0] ? p.in[0][row * p.ldi[0] + c] : 0.f);
+          const float a = p.in[2][row * p.ldi[2] + c];
+          float d1, d2;
+          act_d12(p.act, a, d1, d2);
+          const float hd = d1 * ad + (p.rho != 0.f ? p.rho * p.in[1][row * p.ldi[1] + c] : 0.f);
+          p.out[0][row * p.ldo[0] + c] = ad;
+          p.out[1][row * p.ldo[1] + c] = hd;
+          if (p.last) p.out[2][row * p.ldo[2] + c] = p.vec[0][c] * (p.ubar[row] * d1 + ad * d2);
+        } else if constexpr (EPI == EPI_REV) {
+          const float pn = p.rho == 0.f ? 0.f : (p.in[0] ? p.in[0][row * p.ldi[0] + c] : p.ubar[row] * p.vec[0][c]);
+          const float pv = v + p.rho * pn;
+          const float a = p.in[1][row * p.ldi[1] + c];
+          float d1, d2;
+          act_d12(p.act, a, d1, d2);
+          p.out[0][row * p.ldo[0] + c] = pv;
+          p.out[1][row * p.ldo[1] + c] =
+              pv * d1 + p.in[2][row * p.ldi[2] + c] * p.in[3][row * p.ldi[3] + c] * d2;
+        }
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// u = h . w_out + b_out   (one 16-lane group per row)
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) rowdot_kernel(const float* H, int ldh, int ncols, const float* w,
+                                                     const float* b, float* u, int Rp) {
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int cl = threadIdx.x & 15;
+  if (row >= Rp) return;
+  float s = 0.f;
+  for (int c = cl; c < ncols; c += 16) s += H[(size_t)row * ldh + c] * w[c];
+  s = red16(s);
+  if (cl == 0) u[row] = s + b[0];
+}
+
+// ubar[row] from the per-row residuals; loss partial sums per block.
+// rres[r] = Y_{n+1} - Ytilde_{n+1} (n < N), or Y_N - g(X_N) (n == N).
+__global__ void __launch_bounds__(256) ubar_kernel(const float* rres, const float* xin, int ldx, int R, int Rp,
+                                                   int N1, float phi_r, const float* lossrow, float* ubar,
+                                                   double* loss_part) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  float ub = 0.f;
+  double lv = 0.0;
+  if (row < R) {
+    const int n = row % N1;
+    if (n >= 1) ub += 2.f * rres[row - 1];
+    if (n < N1 - 1) {
+      const float dt = xin[(size_t)(row + 1) * ldx] - xin[(size_t)row * ldx];
+      ub += -2.f * rres[row] * (1.f + phi_r * dt);
+    } else {
+      ub += 2.f * rres[row];
+    }
+    lv = (double)lossrow[row];
+  }
+  if (row < Rp) ubar[row] = ub;
+  __shared__ double red[256];
+  red[threadIdx.x] = lv;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss_part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) loss_final_kernel(const double* part, int n, float* loss) {
+  __shared__ double red[256];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) a += part[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = (float)red[0];
+}
+
+// --------------------------------------------------------------------------
+// TN reduction GEMM for parameter gradients:
+//   C[m, n] = sum_r A0[r, m] B0[r, n] + A1[r, m] B1[r, n]
+// split over r into slabs; 64x64 output tile per workgroup (4 waves of 32x32).
+// --------------------------------------------------------------------------
+struct TNProb {
+  const float* A[2];
+  int lda[2], nA[2];
+  const float* B[2];
+  int ldb[2], nB[2];
+  int npairs;
+  int ones_col;   // pair-0 B column treated as 1.0 (bias gradient); -1 none
+  int mt, nt;     // tiles of 64
+  float* slab;    // [splits][mt*64][nt*64]
+};
+struct TNArgs {
+  TNProb prob[8];
+  int rows_per_split;
+  int Rp;
+};
+
+constexpr int TN_KC = 16;
+constexpr int TN_LS = 80;
+
+__global__ void __launch_bounds__(256) tn_gemm_kernel(TNArgs args) {
+  const TNProb& P = args.prob[blockIdx.z];
+  const int tile = blockIdx.x;
+  if (tile >= P.mt * P.nt) return;
+  const int tm = tile / P.nt, tn = tile - tm * P.nt;
+  const int split = blockIdx.y;
+  const int r_begin = split * args.rows_per_split;
+  int r_end = r_begin + args.rows_per_split;
+  if (r_end > args.Rp) r_end = args.Rp;
+  __shared__ float As[2][TN_KC * TN_LS];
+  __shared__ float Bs[2][TN_KC * TN_LS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  floatx4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = tid >> 4, lc = (tid & 15) * 4;  // loader: row in chunk, col (float4)
+  const int nch = (r_end > r_begin) ? (r_end - r_begin) / TN_KC : 0;
+  const int total = nch * P.npairs;
+  floatx4 ar, br;
+  auto gload = [&](int it) {
+    const int pr = it / nch, ch = it - pr * nch;
+    const size_t r = (size_t)(r_begin + ch * TN_KC + lr);
+    const int ca = tm * 64 + lc, cb = tn * 64 + lc;
+    ar = (ca < P.nA[pr]) ? *(const floatx4*)(P.A[pr] + r * P.lda[pr] + ca) : floatx4{0.f, 0.f, 0.f, 0.f};
+    if (cb < P.nB[pr]) {
+      br = *(const floatx4*)(P.B[pr] + r * P.ldb[pr] + cb);
+    } else {
+      br = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (pr == 0 && P.ones_col >= cb && P.ones_col < cb + 4) br[P.ones_col - cb] = 1.f;
+    }
+  };
+  auto sstore = [&](int buf) {
+    *(floatx4*)&As[buf][lr * TN_LS + lc] = ar;
+    *(floatx4*)&Bs[buf][lr * TN_LS + lc] = br;
+  };
+  if (total > 0) {
+    gload(0);
+    sstore(0);
+    __syncthreads();
+    for (int it = 0; it < total; ++it) {
+      const int buf = it & 1;
+      if (it + 1 < total) gload(it + 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 4 * i + (lane >> 4);
+        float a[2], b[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          a[s] = As[buf][k * TN_LS + wm * 32 + s * 16 + (lane & 15)];
+          b[s] = Bs[buf][k * TN_LS + wn * 32 + s * 16 + (lane & 15)];
+        }
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y) acc[x][y] = mfma4(a[x], b[y], acc[x][y]);
+      }
+      if (it + 1 < total) sstore(buf ^ 1);
+      __syncthreads();
+    }
+  }
+  const int ldc = P.nt * 64;
+  float* C = P.slab + (size_t)split * (P.mt * 64) * ldc;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = tm * 64 + wm * 32 + x * 16 + (lane >> 4) * 4 + j;
+        const int n = tn * 64 + wn * 32 + y * 16 + (lane & 15);
+        C[(size_t)m * ldc + n] = acc[x][y][j];
+      }
+}
+
+// column sums for the output layer: slab[s][c] = sum_r ubar[r]*H[r,c] + Hd[r,c]
+// (c < ncols), slab[s][ncols] = sum_r ubar[r]
+__global__ void __launch_bounds__(256) outgrad_kernel(const float* ubar, const float* H, const float* Hd, int ldh,
+                                                      int ncols, int rows_per_split, int Rp, int ldslab,
+                                                      float* slab) {
+  const int split = blockIdx.x;
+  const int r0 = split * rows_per_split;
+  int r1 = r0 + rows_per_split;
+  if (r1 > Rp) r1 = Rp;
+  for (int c = threadIdx.x; c <= ncols; c += 256) {
+    float s = 0.f;
+    if (c < ncols) {
+      for (int r = r0; r < r1; ++r) s += ubar[r] * H[(size_t)r * ldh + c] + Hd[(size_t)r * ldh + c];
+    } else {
+      for (int r = r0; r < r1; ++r) s += ubar[r];
+    }
+    slab[(size_t)split * ldslab + c] = s;
+  }
+}
+
+// --------------------------------------------------------------------------
+// Descriptor-driven gather/scatter (weight packing, gradient finalize)
+// --------------------------------------------------------------------------
+enum PackMode { PK_COPY = 0, PK_ADD2 = 1, PK_NEGPROJ = 2, PK_SLABSUM = 3 };
+struct PackDesc {
+  const float* src;
+  const float* src2;   // PK_ADD2 second source
+  int src_ld, src2_ld;
+  float* dst;
+  int dst_ld;
+  int rows, cols;
+  int transpose;       // dst[c][r] = v(r, c)
+  int mode;
+  float scale;         // PK_COPY / PK_SLABSUM / PK_ADD2 multiplier
+  int nslab;           // PK_SLABSUM: slabs of stride slab_stride
+  long long slab_stride;
+  const double* proj;  // PK_NEGPROJ: [norm, ...] of this block
+};
+
+// --------------------------------------------------------------------------
+// clip_grad_norm_ + Adam/AdamW/SGD (nd_BSPDE_case.py:383-384; torch defaults)
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sqnorm_kernel(const float* g, const unsigned char* used, long long n,
+                                                     double* part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    if (used[i]) s += (double)g[i] * (double)g[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+struct OptArgs {
+  int kind;
+  float lr, beta2, eps, wd, max_norm;
+  float omb1, omb2;           // 1-beta1, 1-beta2 (computed in double, as torch's Python floats)
+  float step_size, bc2_sqrt;  // lr/(1-beta1^t), sqrt(1-beta2^t)
+  int nparts;
+};
+
+__global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float* m, float* v, const unsigned char* used,
+                                                    long long n, const double* part, OptArgs a) {
+  __shared__ float clip_s;
+  if (threadIdx.x == 0) {
+    float coef = 1.f;
+    if (a.max_norm > 0.f) {
+      double s = 0.0;
+      for (int i = 0; i < a.nparts; ++i) s += part[i];
+      const float tot = (float)sqrt(s);
+      coef = a.max_norm / (tot + 1e-6f);
+      if (coef > 1.f) coef = 1.f;
+    }
+    clip_s = coef;
+  }
+  __syncthreads();
+  const float coef = clip_s;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    if (!used[i]) continue;
+    float gi = g[i] * coef;
+    g[i] = gi;
+    float p = prm[i];
+    if (a.kind == 2) {  // SGD
+      if (a.wd != 0.f) gi = gi + a.wd * p;
+      prm[i] = p - a.lr * gi;
+      continue;
+    }
+    if (a.kind == 1) p = p * (1.f - a.lr * a.wd);         // AdamW decoupled decay
+    else if (a.wd != 0.f) gi = gi + a.wd * p;             // Adam L2
+    float mi = m[i];
+    mi = mi + a.omb1 * (gi - mi);                         // exp_avg.lerp_(g, 1-beta1)
+    float vi = v[i] * a.beta2 + a.omb2 * gi * gi;         // mul_(beta2).addcmul_(g, g, 1-beta2)
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
+    prm[i] = p - a.step_size * (mi / denom);              // addcdiv_(m, denom, -step_size)
+  }
+}
+
+// --------------------------------------------------------------------------
+// output export: rows -> reference layouts
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) export_kernel(const float* xin, const float* zfull, int ldx, const float* u,
+                                                     int R, int D, float* X, float* Y, float* Z) {
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= (long long)R * D) return;
+  const long long r = i / D;
+  const int d = (int)(i - r * D);
+  if (X) X[i] = xin[r * ldx + 1 + d];
+  if (Z) Z[i] = zfull[r * ldx + 1 + d];
+  if (Y && d == 0) Y[r] = u[r];
+}
+
+// net_u input rows: xin[r] = [t_r, X_r, 1, 0..]
+__global__ void __launch_bounds__(256) netu_input_kernel(const float* t, const float* X, int R, int D, int ldx,
+                                                         float* xin) {
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= (long long)R * ldx) return;
+  const long long r = i / ldx;
+  const int c = (int)(i - r * ldx);
+  float v = 0.f;
+  if (c == 0) v = t[r];
+  else if (c <= D) v = X[r * D + c - 1];
+  else if (c == D + 1) v = 1.f;
+  xin[i] = v;
+}
+
+}  // namespace dbsde

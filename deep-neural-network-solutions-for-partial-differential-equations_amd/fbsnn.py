@@ -1,0 +1,298 @@
+"""FBSNN: the reference solver class surface, driven by the HIP library.
+
+Drop-in for the FBSNN classes of nd_BSPDE_case.py:126-500 (v2: Mm schedule,
+optimizer menu, grad clipping, min-loss tracking, save/load),
+with_corr_high_dimension_pde.py:132-540 (v3: correlated increments) and,
+via deepbsde.FBSNN, DeepBSDE.py:140-323.  Same constructor arguments, method
+names, return types and attribute names; the work runs in the C ABI of
+include/dbsde.h (one context per GPU).  Subclasses declare their problem
+coefficients with `problem_spec()` (see problems.py); a subclass that only
+overrides phi_tf/g_tf/mu_tf/sigma_tf cannot run on the native path and is
+rejected at construction.
+
+Multi-GPU: when torch.distributed is initialised (one process per GPU), the
+M paths of every minibatch are split into contiguous blocks of M/world per
+rank; gradients and loss are summed with one all-reduce per step and the
+optimizer runs replicated.
+"""
+from __future__ import annotations
+
+import os
+import time
+from abc import ABC
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import networks
+from .solver import NativeSolver, ProblemSpec
+
+OPTIMIZER_NAMES = ("Adam", "SGD", "RMSprop", "AdamW", "Adadelta", "Adagrad", "Adamax", "ASGD", "LBFGS")
+NATIVE_OPTIMIZERS = ("Adam", "AdamW", "SGD")
+
+
+def _default_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("the native deep-BSDE path needs a HIP device; none is visible")
+    return torch.device("cuda", int(os.environ.get("LOCAL_RANK", torch.cuda.current_device())))
+
+
+def _world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+class FBSNN(ABC):
+    """nd_BSPDE_case.py:126 / with_corr_high_dimension_pde.py:132 surface."""
+
+    # reference behaviour switches (nd v2 defaults)
+    clip_max_norm = 1.0          # nd_BSPDE_case.py:383 (DeepBSDE: none)
+    schedule = "nd"              # Q1: "nd" (nd_BSPDE_case.py:364-368), "corr" (with_corr:406-409) or None
+    log_every = 100
+
+    def __init__(self, Xi, T, M, N, D, Mm, layers, mode, activation, correlation_type="no_correlation",
+                 device=None):
+        self.device = torch.device(device) if device is not None else _default_device()
+        self.Xi = torch.as_tensor(np.asarray(Xi), dtype=torch.float32).to(self.device)
+        self.T, self.M, self.N, self.D, self.Mm = T, M, N, D, Mm
+        self.strike = self._default_strike()
+        self.mode, self.activation = mode, activation
+        self.layers = list(layers)
+        spec = self.problem_spec()
+        if not isinstance(spec, ProblemSpec):
+            raise NotImplementedError(
+                f"{type(self).__name__} does not declare problem_spec(); custom phi_tf/g_tf/mu_tf/"
+                "sigma_tf cannot run on the native path")
+        self.spec = spec
+        self.solver = NativeSolver(mode, self.layers, activation, spec, T, self.device)
+        self.model = networks.make_model(mode, self.layers, activation)
+        self.params = networks.flatten_into(self.model, self.device)
+        if self.params.numel() != self.solver.nparams:
+            raise RuntimeError("native parameter layout does not match the module layout")
+        self.grad = torch.zeros_like(self.params)
+        self.training_loss = []
+        self.iteration = []
+        self.correlation_type = correlation_type
+        self.correlation_matrix = self.generate_correlation_matrix(D)
+        self._L = None if correlation_type == "no_correlation" else np.linalg.cholesky(self.correlation_matrix)
+        self.rank, self.world = _world()
+
+    # ------------------------------------------------------------------ problem
+    def _default_strike(self):
+        return 1.0 * self.D          # nd_BSPDE_case.py:147
+
+    def problem_spec(self):
+        return None
+
+    def phi_tf(self, t, X, Y, Z):
+        raise NotImplementedError
+
+    def g_tf(self, X):
+        raise NotImplementedError
+
+    def mu_tf(self, t, X, Y, Z):
+        return torch.zeros([X.shape[0], self.D], device=X.device)
+
+    def sigma_tf(self, t, X, Y):
+        return torch.diag_embed(torch.ones([X.shape[0], self.D], device=X.device))
+
+    # ------------------------------------------------------------------ correlation (with_corr:186-212)
+    def generate_correlation_matrix(self, D):
+        ct = getattr(self, "correlation_type", "no_correlation")
+        if ct == "no_correlation":
+            return np.eye(D)
+        if ct == "random_correlation":
+            return self._random_corr(D, False)
+        if ct == "restricted_random_correlation":
+            return self._random_corr(D, True)
+        raise ValueError("Invalid correlation type")
+
+    @staticmethod
+    def _random_corr(D, positive):
+        a = np.random.randn(D, D)
+        if positive:
+            a = np.abs(a)
+        c = a @ a.T
+        np.fill_diagonal(c, 1)          # before the normalisation, as the reference does (Q10)
+        d = np.sqrt(np.diag(c))
+        c = c / np.outer(d, d)
+        eps = 1e-6
+        while not np.all(np.linalg.eigvals(c) > 0):
+            c += eps * np.eye(D)
+            eps *= 2
+        return c
+
+    # ------------------------------------------------------------------ solver core
+    def fetch_minibatch(self):
+        """DeepBSDE.py:247-262 / with_corr:316-353: host numpy draws (the parity
+        stream), returned on the device."""
+        M, N, D, T = self.M, self.N, self.D, self.T
+        Dt = np.zeros((M, N + 1, 1))
+        DW = np.zeros((M, N + 1, D))
+        dt = T / N
+        Dt[:, 1:, :] = dt
+        dw = np.sqrt(dt) * np.random.normal(size=(M, N, D))
+        DW[:, 1:, :] = dw if self._L is None else np.einsum('ij,mnj->mni', self._L, dw)
+        t = torch.from_numpy(np.cumsum(Dt, axis=1)).float().to(self.device)
+        W = torch.from_numpy(np.cumsum(DW, axis=1)).float().to(self.device)
+        return t, W
+
+    def _xi_rows(self, Xi, M):
+        Xi = torch.as_tensor(Xi, dtype=torch.float32).to(self.device).reshape(-1, self.D).contiguous()
+        if Xi.shape[0] not in (1, M):
+            raise ValueError(f"Xi has {Xi.shape[0]} rows; expected 1 or {M}")
+        return Xi
+
+    def _run(self, t, W, Xi, grad=None, want=("X", "Y")):
+        """One native loss(+grad) evaluation over the paths of t/W."""
+        M, N1 = t.shape[0], t.shape[1]
+        N = N1 - 1
+        Xi = self._xi_rows(Xi, M)
+        out = {"loss": torch.empty(1, device=self.device)}
+        if "X" in want:
+            out["X"] = torch.empty((M, N1, self.D), device=self.device)
+        if "Y" in want:
+            out["Y"] = torch.empty((M, N1, 1), device=self.device)
+        if "Z" in want:
+            out["Z"] = torch.empty((M, N1, self.D), device=self.device)
+        self.solver.loss_grad(self.params, M, N, Xi, t=t.reshape(M, N1).contiguous().float(),
+                              W=W.reshape(M, N1, self.D).contiguous().float(), grad=grad, loss=out["loss"],
+                              X=out.get("X"), Y=out.get("Y"), Z=out.get("Z"))
+        return out
+
+    def net_u(self, t, X):
+        """DeepBSDE.py:189-194: (u [R,1], Du [R,D]) at the given points."""
+        X = torch.as_tensor(X, dtype=torch.float32).to(self.device)
+        if X.dim() == 1:
+            X = X.unsqueeze(-1)
+        t = torch.as_tensor(t, dtype=torch.float32).to(self.device).reshape(-1).contiguous()
+        X = X.reshape(-1, self.D).contiguous()
+        u = torch.empty((X.shape[0], 1), device=self.device)
+        du = torch.empty_like(X)
+        self.solver.net_u(self.params, t, X, u, du)
+        return u, du
+
+    def Dg_tf(self, X):
+        """DeepBSDE.py:196-200 (torch autograd of the problem's g_tf)."""
+        X = X.detach().requires_grad_(True)
+        g = self.g_tf(X)
+        return torch.autograd.grad(g, X, torch.ones_like(g))[0]
+
+    def loss_function(self, t, W, Xi):
+        """nd_BSPDE_case.py:237-281 -> (loss, X, Y, Y[0,0,0])."""
+        out = self._run(t, W, Xi)
+        Y = out["Y"]
+        return out["loss"][0], out["X"], Y, Y[0, 0, 0]
+
+    # ------------------------------------------------------------------ training
+    def _schedule_n(self, it):
+        if self.schedule == "nd" and self.Mm is not None:
+            if 4000 <= it < 20000:
+                self.N = int(np.ceil(self.Mm ** (int(it / 4000) + 1)))
+            elif it < 4000:
+                self.N = int(np.ceil(self.Mm))
+        elif self.schedule == "corr":
+            if 4000 <= it < 20000:
+                self.N = int(np.ceil((self.N ** (1 / 5)) ** (int(it / 4000) + 1)))
+            elif it < 4000:
+                self.N = int(np.ceil(self.N ** (1 / 5)))
+
+    def _local_slice(self, M):
+        if self.world == 1:
+            return 0, M
+        if M % self.world:
+            raise ValueError(f"M={M} is not divisible by the world size {self.world}")
+        m = M // self.world
+        return self.rank * m, m
+
+    def train_step(self, t, W, opt_state, optimizer_type, learning_rate, want_state=False):
+        """fetch -> loss/grad -> all-reduce -> clip -> optimizer step, on the
+        local shard of the minibatch.  Returns the device loss (and X, Y)."""
+        p0, ml = self._local_slice(t.shape[0])
+        xi = self.Xi if self.Xi.reshape(-1, self.D).shape[0] == 1 else self.Xi.reshape(-1, self.D)[p0:p0 + ml]
+        out = self._run(t[p0:p0 + ml], W[p0:p0 + ml], xi, grad=self.grad,
+                        want=("X", "Y") if want_state else ())
+        loss = out["loss"]
+        if self.world > 1:
+            buf = torch.cat([self.grad, loss])
+            dist.all_reduce(buf)
+            self.grad.copy_(buf[:-1])
+            loss = buf[-1:]
+        opt_state["step"] += 1
+        self.solver.optimizer_step(self.params, self.grad, opt_state["m"], opt_state["v"], kind=optimizer_type,
+                                   lr=learning_rate, max_norm=self.clip_max_norm or 0.0,
+                                   step=opt_state["step"])
+        return loss, out
+
+    def _check_optimizer(self, optimizer_type):
+        if optimizer_type not in OPTIMIZER_NAMES:
+            raise ValueError(f"Optimizer type '{optimizer_type}' is not recognized.")
+        if optimizer_type not in NATIVE_OPTIMIZERS:
+            raise NotImplementedError(f"optimizer {optimizer_type!r} has no native implementation yet "
+                                      f"(available: {', '.join(NATIVE_OPTIMIZERS)})")
+
+    def new_optimizer_state(self):
+        return {"m": torch.zeros_like(self.params), "v": torch.zeros_like(self.params), "step": 0}
+
+    def train(self, N_Iter, learning_rate, optimizer_type='Adam'):
+        """nd_BSPDE_case.py:316-410 -> (graph, min_loss, min_loss_state)."""
+        self._check_optimizer(optimizer_type)
+        loss_temp = []
+        previous_it = self.iteration[-1] if self.iteration else 0
+        opt_state = self.new_optimizer_state()    # a fresh optimizer per call (Q11)
+        start_time = time.time()
+        min_loss, min_loss_state = float('inf'), None
+        for it in range(previous_it, previous_it + N_Iter):
+            self._schedule_n(it)
+            t_batch, W_batch = self.fetch_minibatch()
+            loss_t, out = self.train_step(t_batch, W_batch, opt_state, optimizer_type, learning_rate,
+                                          want_state=True)
+            loss = float(loss_t.item())
+            loss_temp.append(loss)
+            if loss < min_loss:
+                min_loss = loss
+                min_loss_state = (out["X"].clone(), out["Y"].clone())
+            if it % self.log_every == 0:
+                elapsed = time.time() - start_time
+                if self.rank == 0:
+                    y0 = float(out["Y"][0, 0, 0])
+                    print(f'It: {it}, Loss: {loss:.3e}, Y0: {y0:.3f}, Time: {elapsed:.2f}, '
+                          f'Learning Rate: {learning_rate:.3e}')
+                start_time = time.time()
+                self.training_loss.append(float(np.mean(loss_temp)))
+                loss_temp = []
+                self.iteration.append(it)
+        graph = np.stack((self.iteration, self.training_loss))
+        return graph, min_loss, min_loss_state
+
+    # ------------------------------------------------------------------ inference
+    def predict(self, Xi_star, t_star, W_star):
+        """nd_BSPDE_case.py:412-443 (sets self.M to the batch size)."""
+        Xi_star = torch.as_tensor(np.asarray(Xi_star) if not isinstance(Xi_star, torch.Tensor) else Xi_star,
+                                  dtype=torch.float32).to(self.device).reshape(-1, self.D)
+        t_star = torch.as_tensor(t_star, dtype=torch.float32).to(self.device)
+        W_star = torch.as_tensor(W_star, dtype=torch.float32).to(self.device)
+        bs = max(Xi_star.shape[0], t_star.shape[0], W_star.shape[0])
+        self.M = bs
+        if t_star.shape[0] == 1:
+            t_star = t_star.repeat(bs, 1, 1)
+        if W_star.shape[0] == 1:
+            W_star = W_star.repeat(bs, 1, 1)
+        out = self._run(t_star, W_star, Xi_star)
+        return out["X"], out["Y"]
+
+    # ------------------------------------------------------------------ checkpoints
+    def save_model(self, file_name):
+        torch.save({'model_state_dict': self.model.state_dict(), 'training_loss': self.training_loss,
+                    'iteration': self.iteration}, file_name)
+
+    def load_model(self, file_name):
+        ck = torch.load(file_name, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(ck['model_state_dict'])
+        self.training_loss = list(ck['training_loss'])
+        self.iteration = list(ck['iteration'])
+
+
+__all__ = ["FBSNN", "ProblemSpec", "OPTIMIZER_NAMES", "NATIVE_OPTIMIZERS"]

@@ -1,0 +1,162 @@
+"""NativeSolver: one C-ABI context (one GPU) driving the HIP deep-BSDE step.
+
+torch is used only as device-memory/stream plumbing: tensors are handed to
+the library as raw device pointers (data_ptr) and kernels are enqueued on
+torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class ProblemSpec:
+    """Coefficients of one reference FBSNN subclass (see include/dbsde.h):
+    mu = mu_a X, sigma = diag(sig_a X + sig_b), phi = phi_r (Y - phi_c X.Z) + phi_zz |Z|^2,
+    g = g_kind(strike).  q3: reproduce the D == 1 squeeze broadcast."""
+
+    mu_a: float = 0.0
+    sig_a: float = 0.0
+    sig_b: float = 0.0
+    phi_r: float = 0.0
+    phi_c: float = 0.0
+    phi_zz: float = 0.0
+    g: str = "sumsq"
+    strike: float = 0.0
+    q3: bool = True
+
+    def to_c(self):
+        if self.g not in _lib.G_KINDS:
+            raise ValueError(f"unknown terminal condition {self.g!r}")
+        return _lib.Problem(self.mu_a, self.sig_a, self.sig_b, self.phi_r, self.phi_c, self.phi_zz,
+                            _lib.G_KINDS[self.g], self.strike, int(self.q3))
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class NativeSolver:
+    """Owns one dbsde_ctx.  All tensors must be float32, contiguous, on `device`."""
+
+    def __init__(self, mode, layers, activation, problem: ProblemSpec, T, device):
+        if mode not in _lib.MODES:
+            raise ValueError(f"mode {mode!r} is not one of {sorted(_lib.MODES)}")
+        if activation not in _lib.ACTIVATIONS:
+            raise ValueError(f"activation {activation!r} is not one of {sorted(_lib.ACTIVATIONS)}")
+        if len(layers) > 16:
+            raise ValueError("at most 16 layer widths are supported")
+        self.lib = _lib.load()
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("the native deep-BSDE path needs a HIP device (torch 'cuda' device)")
+        cfg = _lib.Config()
+        cfg.mode = _lib.MODES[mode]
+        cfg.activation = _lib.ACTIVATIONS[activation]
+        cfg.n_layers = len(layers)
+        for k, v in enumerate(layers):
+            cfg.layers[k] = int(v)
+        cfg.problem = problem.to_c()
+        cfg.T = float(T)
+        cfg.device = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        ctx = ctypes.c_void_p()
+        _lib.check(self.lib.dbsde_create(ctypes.byref(cfg), ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.layers = list(layers)
+        self.D = layers[0] - 1
+        self.nparams = int(self.lib.dbsde_param_count(ctx))
+        mask = (ctypes.c_ubyte * self.nparams)()
+        _lib.check(self.lib.dbsde_param_used_mask(ctx, mask, self.nparams), ctx)
+        self.used_mask = torch.frombuffer(bytearray(mask), dtype=torch.uint8).bool()
+
+    def __del__(self):
+        ctx = getattr(self, "ctx", None)
+        if ctx is not None and ctx.value:
+            try:
+                self.lib.dbsde_destroy(ctx)
+            except Exception:
+                pass
+            self.ctx = None
+
+    # ------------------------------------------------------------------
+    def _check_tensor(self, t, name, numel=None):
+        if t is None:
+            return
+        if not isinstance(t, torch.Tensor) or t.device != self.device or t.dtype != torch.float32:
+            raise ValueError(f"{name} must be a float32 tensor on {self.device}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        if numel is not None and t.numel() != numel:
+            raise ValueError(f"{name} has {t.numel()} elements, expected {numel}")
+
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(self.lib.dbsde_set_stream(self.ctx, ctypes.c_void_p(s)), self.ctx)
+
+    def loss_grad(self, params, M, N, Xi, t=None, W=None, seed=0, offset=0, path0=0, grad=None, loss=None,
+                  X=None, Y=None, Z=None):
+        """FBSNN.loss_function (+ loss.backward when grad is given)."""
+        D = self.D
+        self._check_tensor(params, "params", self.nparams)
+        self._check_tensor(grad, "grad", self.nparams)
+        self._check_tensor(Xi, "Xi")
+        if Xi.numel() not in (D, M * D):
+            raise ValueError("Xi must hold 1 or M rows of D values")
+        self._check_tensor(t, "t", M * (N + 1))
+        self._check_tensor(W, "W", M * (N + 1) * D)
+        self._check_tensor(loss, "loss", 1)
+        self._check_tensor(X, "X", M * (N + 1) * D)
+        self._check_tensor(Y, "Y", M * (N + 1))
+        self._check_tensor(Z, "Z", M * (N + 1) * D)
+        b = _lib.Batch(int(M), int(N), _ptr(t), _ptr(W), int(seed) & (2 ** 64 - 1),
+                       int(offset) & (2 ** 64 - 1), int(path0), _ptr(Xi), Xi.numel() // D)
+        o = _lib.Outputs(_ptr(loss), _ptr(X), _ptr(Y), _ptr(Z))
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_loss_grad(self.ctx, _ptr(params), ctypes.byref(b), _ptr(grad),
+                                            ctypes.byref(o)), self.ctx)
+
+    def net_u(self, params, t, X, u, Du):
+        R = X.numel() // self.D
+        self._check_tensor(params, "params", self.nparams)
+        for name, v, n in (("t", t, R), ("X", X, R * self.D), ("u", u, R), ("Du", Du, R * self.D)):
+            self._check_tensor(v, name, n)
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_net_u(self.ctx, _ptr(params), R, _ptr(t), _ptr(X), _ptr(u), _ptr(Du)),
+                   self.ctx)
+
+    def optimizer_step(self, params, grad, m, v, kind="Adam", lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                       weight_decay=0.0, max_norm=0.0, step=1):
+        if kind not in _lib.OPTIMIZERS:
+            raise ValueError(f"Optimizer type '{kind}' is not recognized.")
+        for name, v_ in (("params", params), ("grad", grad), ("m", m), ("v", v)):
+            self._check_tensor(v_, name, self.nparams)
+        o = _lib.Optim(_lib.OPTIMIZERS[kind], lr, betas[0], betas[1], eps, weight_decay,
+                       max_norm if max_norm else 0.0, int(step))
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_optimizer_step(self.ctx, _ptr(params), _ptr(grad), _ptr(m), _ptr(v),
+                                                 ctypes.byref(o)), self.ctx)
+
+    # ------------------------------------------------------------------ profiling
+    def profile(self, enable=True):
+        _lib.check(self.lib.dbsde_profile_enable(self.ctx, int(enable)), self.ctx)
+
+    def profile_reset(self):
+        _lib.check(self.lib.dbsde_profile_reset(self.ctx), self.ctx)
+
+    def profile_read(self):
+        n = self.lib.dbsde_profile_count(self.ctx)
+        if n < 0:
+            _lib.check(n, self.ctx)
+        out = {}
+        name = ctypes.create_string_buffer(128)
+        ms, fl, by, nl = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
+        for i in range(n):
+            _lib.check(self.lib.dbsde_profile_read(self.ctx, i, name, 128, ctypes.byref(ms), ctypes.byref(fl),
+                                                   ctypes.byref(by), ctypes.byref(nl)), self.ctx)
+            out[name.value.decode()] = dict(ms=ms.value, flops=fl.value, bytes=by.value, launches=nl.value)
+        return out

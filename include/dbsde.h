@@ -1,0 +1,168 @@
+/*
+ * dbsde.h -- C ABI of the MI355X-native deep-BSDE training step.
+ *
+ * This is the drop-in boundary for the reference's FBSNN solver surface
+ * (nd_BSPDE_case.py:126-500, DeepBSDE.py:140-323).  Every entry point below
+ * replaces one reference method; the Python binding that a maintainer adds
+ * to a reference-style script is the ctypes class in
+ * deep-neural-network-solutions-for-partial-differential-equations_amd/fbsnn.py
+ * (see INTEGRATION.md).
+ *
+ * Conventions
+ *   - Every function returns 0 on success and a negative DBSDE_E* code on
+ *     failure; dbsde_last_error() then holds a message.
+ *   - Pointers documented as "device" are HIP device pointers on the
+ *     context's device (e.g. torch.Tensor.data_ptr() of a cuda tensor).
+ *   - Parameters, gradients and optimizer moments are FLAT fp32 vectors in
+ *     the reference module's state_dict() order (nd_BSPDE_case.py:445-456
+ *     save format), so torch checkpoints interoperate.
+ *   - Work is enqueued on the stream set by dbsde_set_stream (default: the
+ *     legacy null stream) and is asynchronous: results are valid once the
+ *     stream has been synchronised.  The context keeps no caller pointer
+ *     after a call returns.  A context is not thread safe.
+ */
+#ifndef DBSDE_H
+#define DBSDE_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DBSDE_ABI_VERSION 1
+
+/* error codes */
+#define DBSDE_OK 0
+#define DBSDE_EINVAL -1   /* bad configuration or argument (Python: ValueError)   */
+#define DBSDE_EHIP -2     /* HIP runtime failure             (Python: RuntimeError) */
+#define DBSDE_ENOMEM -3   /* device allocation failed        (Python: MemoryError)  */
+
+/* network modes: DeepBSDE.py:166-178, nd_BSPDE_case.py:159-172 */
+#define DBSDE_MODE_FC 0        /* "FC"       nn.Sequential of Linear/act            */
+#define DBSDE_MODE_NAIS_NET 1  /* "NAIS-Net" Resnet(stable=True), DeepBSDE.py:23-65 */
+#define DBSDE_MODE_RESNET 2    /* "Resnet"   Resnet(stable=False)                   */
+#define DBSDE_MODE_NAISNET 3   /* "Naisnet"  Functions/naisnet.py:6-96              */
+
+/* activations: Functions/Sine.py, nn.ReLU, nn.Tanh */
+#define DBSDE_ACT_SINE 0
+#define DBSDE_ACT_RELU 1
+#define DBSDE_ACT_TANH 2
+
+/* terminal conditions g(X) */
+#define DBSDE_G_SUMSQ 0      /* sum X^2                 DeepBSDE.py:333-335          */
+#define DBSDE_G_CALL_SUM 1   /* max(sum X - K, 0)       nd_BSPDE_case.py:521-522     */
+#define DBSDE_G_CALL_MEAN 2  /* max(mean X - K, 0)      with_corr...py:577-579       */
+#define DBSDE_G_LOG 3        /* log(1/2 + 1/2 sum X^2)  hjb_implement.py:597-598     */
+
+/*
+ * Problem coefficients (one FBSNN subclass = one filled struct):
+ *   mu(X)    = mu_a * X                                  (diagonal drift)
+ *   sigma(X) = diag(sig_a * X + sig_b)                   (the reference's
+ *                                                          dense diag_embed sigma)
+ *   phi      = phi_r * (Y - phi_c * X.Z) + phi_zz * |Z|^2
+ *   g        = g_kind with strike
+ *   q3       = 1: for D == 1 reproduce the reference's squeeze() broadcast in
+ *              the Y-tilde term (1d_BSPDE_case.py:271-273)
+ */
+typedef struct dbsde_problem {
+  float mu_a, sig_a, sig_b;
+  float phi_r, phi_c, phi_zz;
+  int g_kind;
+  float strike;
+  int q3;
+} dbsde_problem;
+
+typedef struct dbsde_config {
+  int mode;          /* DBSDE_MODE_*                                   */
+  int activation;    /* DBSDE_ACT_*                                    */
+  int n_layers;      /* len(layers), 3..16                             */
+  int layers[16];    /* [D+1, W1, ..., Wk, 1]                          */
+  dbsde_problem problem;
+  float T;           /* terminal time                                  */
+  int device;        /* HIP device ordinal                             */
+} dbsde_config;
+
+typedef struct dbsde_ctx dbsde_ctx;
+
+/* FBSNN.__init__ (network/problem construction; weights are caller-owned) */
+int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out);
+void dbsde_destroy(dbsde_ctx* ctx);
+const char* dbsde_last_error(const dbsde_ctx* ctx); /* ctx may be NULL */
+int dbsde_abi_version(void);
+int dbsde_set_stream(dbsde_ctx* ctx, void* hip_stream);
+
+/* size of the flat parameter vector = sum of state_dict numels */
+long long dbsde_param_count(const dbsde_ctx* ctx);
+/* host mask[i] = 1 if parameter element i receives a gradient (SURVEY Q6:
+ * Resnet(stable) input_layers[-1] is never used and stays grad=None) */
+int dbsde_param_used_mask(const dbsde_ctx* ctx, unsigned char* mask, long long n);
+
+/*
+ * One minibatch (FBSNN.fetch_minibatch output, DeepBSDE.py:247-262).
+ *   W != NULL : parity mode, t [M,N+1] and W [M,N+1,D] device fp32 exactly as
+ *               the reference builds them (cumsum in fp64, cast).
+ *   W == NULL : device mode, Brownian increments sqrt(dt)*N(0,1) drawn by an
+ *               in-kernel Philox4x32-10 keyed by (seed, offset, global path,
+ *               step, dim); t == NULL means the uniform grid T*n/N.
+ *               A rank holding paths [path0, path0+M) of a larger batch draws
+ *               exactly the increments a single device would draw for them.
+ */
+typedef struct dbsde_batch {
+  int M, N;
+  const float* t;
+  const float* W;
+  unsigned long long seed, offset;
+  long long path0;   /* global index of local path 0 (Philox stream of a rank's shard) */
+  const float* Xi;   /* device [xi_rows, D], xi_rows in {1, M} */
+  int xi_rows;
+} dbsde_batch;
+
+typedef struct dbsde_outputs {
+  float* loss;   /* device scalar, nullable        */
+  float* X;      /* device [M, N+1, D], nullable   */
+  float* Y;      /* device [M, N+1], nullable      */
+  float* Z;      /* device [M, N+1, D], nullable   */
+} dbsde_outputs;
+
+/*
+ * FBSNN.loss_function + loss.backward (DeepBSDE.py:202-245, 279).
+ * grad (device, flat, param_count) receives d loss / d params (overwritten,
+ * 0 for unused parameters); grad == NULL runs the forward only (predict,
+ * nd_BSPDE_case.py:412-443).
+ */
+int dbsde_loss_grad(dbsde_ctx* ctx, const float* params, const dbsde_batch* batch,
+                    float* grad, const dbsde_outputs* out);
+
+/* FBSNN.net_u (DeepBSDE.py:189-194): u [R] and Du [R,D] at R points. */
+int dbsde_net_u(dbsde_ctx* ctx, const float* params, int R, const float* t,
+                const float* X, float* u, float* Du);
+
+/* optimizers (nd_BSPDE_case.py:331-350) */
+#define DBSDE_OPT_ADAM 0
+#define DBSDE_OPT_ADAMW 1
+#define DBSDE_OPT_SGD 2
+
+typedef struct dbsde_optim {
+  int kind;
+  float lr, beta1, beta2, eps, weight_decay;
+  float max_norm;    /* clip_grad_norm_(max_norm) before the step; <= 0: no clip */
+  long long step;    /* 1-based step count of THIS update (bias correction) */
+} dbsde_optim;
+
+/* clip_grad_norm_ + optimizer.step() (nd_BSPDE_case.py:383-384); m, v device
+ * flat moments owned by the caller (zero-initialised for a fresh optimizer). */
+int dbsde_optimizer_step(dbsde_ctx* ctx, float* params, float* grad, float* m, float* v,
+                         const dbsde_optim* opt);
+
+/* Per-kernel timing with HIP events on the context stream (bench/profiling). */
+int dbsde_profile_enable(dbsde_ctx* ctx, int enable);
+int dbsde_profile_count(dbsde_ctx* ctx);
+int dbsde_profile_read(dbsde_ctx* ctx, int idx, char* name, int name_len, double* total_ms,
+                       double* alg_flops, double* alg_bytes, long long* launches);
+int dbsde_profile_reset(dbsde_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DBSDE_H */

@@ -1,0 +1,225 @@
+"""Generate the golden parity vectors by running the REFERENCE itself.
+
+Run in the build container only (it reads /root/reference, which the GPU box
+does not have):   python tests/golden/make_golden.py
+The outputs (tests/golden/*.npz) are data -- inputs and the reference's
+outputs -- and are what the oracle and the HIP path are checked against.
+
+Each case seeds torch and numpy, constructs the reference problem class
+(so the reference's own init runs), draws the reference's own minibatch,
+runs the reference loss_function and loss.backward(), and stores
+  params (flat, state_dict order), t, W, Xi, loss, X, Y, Z (via the
+  reference net_u on the reference X), grad (flat) and used-mask.
+Training cases additionally run the reference train() and store the final
+parameters.  seaborn is not installed here; the reference imports it only for
+plotting, so an empty stub module is registered.
+"""
+from __future__ import annotations
+
+import contextlib
+import importlib.util
+import io
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _load(fname, modname):
+    spec = importlib.util.spec_from_file_location(modname, os.path.join(REF, fname))
+    mod = importlib.util.module_from_spec(spec)
+    with contextlib.redirect_stdout(io.StringIO()):
+        spec.loader.exec_module(mod)
+    return mod
+
+
+def _setup():
+    import matplotlib
+    matplotlib.use("Agg")
+    sys.modules.setdefault("seaborn", types.ModuleType("seaborn"))
+    sys.path.insert(0, REF)
+    mods = dict(
+        deep=_load("DeepBSDE.py", "ref_DeepBSDE"),
+        nd=_load("nd_BSPDE_case.py", "ref_nd"),
+        corr=_load("with_corr_high_dimension_pde.py", "ref_corr"),
+        hjb=_load("hjb_implement.py", "ref_hjb"),
+        oned=_load("1d_BSPDE_case.py", "ref_1d"),
+    )
+    import torch
+    torch.autograd.set_detect_anomaly(False)   # DeepBSDE.py:11 turns it on (Q8); speed only
+    torch.set_num_threads(1)                  # deterministic reductions
+    return mods
+
+
+def _flat(sd):
+    import torch
+    return torch.cat([p.detach().reshape(-1) for p in sd.values()]).numpy().astype(np.float32)
+
+
+def _grads(model):
+    params = dict(model.named_parameters())
+    g, m = [], []
+    for name, p in model.state_dict().items():
+        q = params[name]
+        if q.grad is None:
+            g.append(np.zeros(q.numel(), np.float32))
+            m.append(np.zeros(q.numel(), bool))
+        else:
+            g.append(q.grad.detach().reshape(-1).numpy())
+            m.append(np.ones(q.numel(), bool))
+    return np.concatenate(g), np.concatenate(m)
+
+
+def _run_case(obj, M, N, D, full_z=True):
+    """Reference minibatch + loss + backward on `obj` (a reference FBSNN)."""
+    import torch
+    with contextlib.redirect_stdout(io.StringIO()):
+        t, W = obj.fetch_minibatch()
+        obj.model.zero_grad(set_to_none=True)
+        out = obj.loss_function(t, W, obj.Xi)
+        loss, X, Y = out[0], out[1], out[2]
+        loss.backward()
+        g, used = _grads(obj.model)
+        Zs = []
+        if full_z:
+            for n in range(N + 1):
+                Xn = X[:, n, :].detach().clone().requires_grad_(True)
+                _, zn = obj.net_u(t[:, n, :], Xn)
+                Zs.append(zn.detach())
+    res = dict(t=t.numpy(), W=W.numpy(), loss=np.float64(loss.item()),
+               X=X.detach().numpy(), Y=Y.detach().numpy(), grad=g, used=used)
+    if full_z:
+        res["Z"] = torch.stack(Zs, 1).numpy()
+    return res
+
+
+def small_cases(mods):
+    """G1/G3: small shapes over archs x activations x problems (+ quirks)."""
+    import torch
+    T = 1.0
+    cases = []
+    D4 = 4
+    L4 = [D4 + 1, 16, 16, 16, 16, 1]
+    xi_bsb = np.array([1.0, 0.5] * (D4 // 2))[None, :]
+    for mode in ["NAIS-Net", "Resnet", "FC"]:
+        for act in ["Sine", "ReLU"]:
+            cases.append((f"deep_bsb_{mode}_{act}", "deep", "BlackScholesBarenblatt", "bsb", mode, act,
+                          L4, xi_bsb, 8, 5, {}))
+    for mode in ["Naisnet", "FC"]:
+        for act in ["Sine", "ReLU", "Tanh"]:
+            cases.append((f"nd_call_{mode}_{act}", "nd", "CallOption", "call", mode, act,
+                          L4, np.ones((1, D4)), 8, 5, {"Mm": 5.0}))
+    cases.append(("nd_call_Naisnet_Sine_len4", "nd", "CallOption", "call", "Naisnet", "Sine",
+                  [D4 + 1, 16, 16, 1], np.ones((1, D4)), 8, 5, {"Mm": 5.0}))
+    cases.append(("nd_call_Naisnet_Tanh_len5", "nd", "CallOption", "call", "Naisnet", "Tanh",
+                  [D4 + 1, 16, 16, 16, 1], np.ones((1, D4)), 8, 5, {"Mm": 5.0}))
+    cases.append(("corr_basket_Naisnet_ReLU", "corr", "CallOption", "basket", "Naisnet", "ReLU",
+                  L4, np.ones((1, D4)), 8, 5, {"Mm": 5.0, "correlation_type": "random_correlation"}))
+    cases.append(("corr_basket_Naisnet_Sine_restricted", "corr", "CallOption", "basket", "Naisnet", "Sine",
+                  L4, np.ones((1, D4)), 8, 5,
+                  {"Mm": 5.0, "correlation_type": "restricted_random_correlation"}))
+    cases.append(("corr_bspdetest_Naisnet_Sine", "corr", "BSPDETestCase", "bspde_test", "Naisnet", "Sine",
+                  L4, xi_bsb, 8, 5, {"Mm": 5.0}))
+    for mode, act in [("FC", "Sine"), ("Naisnet", "ReLU")]:
+        cases.append((f"hjb_{mode}_{act}", "hjb", "HamiltonJacobiBellman", "hjb", mode, act,
+                      L4, np.zeros((1, D4)), 8, 5, {}))
+    for mode, act, M in [("FC", "Sine", 4), ("Naisnet", "Tanh", 6), ("FC", "ReLU", 1)]:
+        cases.append((f"oned_call_{mode}_{act}_M{M}", "oned", "CallOption", "call1d", mode, act,
+                      [2, 16, 16, 16, 16, 1], np.array([[1.0]]), M, 5, {"Mm": 5.0}))
+
+    for seed, (name, modkey, cls, prob, mode, act, layers, Xi, M, N, kw) in enumerate(cases):
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        C = getattr(mods[modkey], cls)
+        D = layers[0] - 1
+        with contextlib.redirect_stdout(io.StringIO()):
+            if modkey == "deep":
+                obj = C(Xi, T, M, N, D, layers, mode, act)
+            elif modkey == "hjb":
+                obj = C(Xi, T, M, N, D, layers, mode, act)
+            elif modkey == "corr":
+                obj = C(Xi, T, M, N, D, kw["Mm"], layers, mode, act,
+                        kw.get("correlation_type", "no_correlation"))
+            else:
+                obj = C(Xi, T, M, N, D, kw["Mm"], layers, mode, act)
+        params = _flat(obj.model.state_dict())
+        res = _run_case(obj, M, N, D)
+        extra = {}
+        if modkey in ("corr", "hjb"):
+            extra["corr"] = np.asarray(obj.correlation_matrix, np.float64)
+        np.savez_compressed(os.path.join(OUT, f"g1_{name}.npz"), name=name, problem=prob, mode=mode,
+                            activation=act, layers=np.array(layers), Xi=Xi.astype(np.float32),
+                            M=M, N=N, T=T, seed=seed, params=params, **res, **extra)
+        print(f"{name:42s} loss={res['loss']:.6e}")
+
+
+def train_cases(mods):
+    """Reference train() trajectories: DeepBSDE (no clip) and nd (clip 1.0, Mm)."""
+    import torch
+    D = 4
+    layers = [D + 1, 16, 16, 16, 16, 1]
+    specs = [("train_deep_bsb_NAIS-Net_Sine", "deep", "BlackScholesBarenblatt", "bsb", "NAIS-Net", "Sine",
+              np.array([1.0, 0.5] * 2)[None, :], 8, 5, None, 10, 1e-3),
+             ("train_nd_call_Naisnet_Sine", "nd", "CallOption", "call", "Naisnet", "Sine",
+              np.ones((1, D)), 8, 5, 5.0, 10, 1e-3)]
+    for k, (name, modkey, cls, prob, mode, act, Xi, M, N, Mm, iters, lr) in enumerate(specs):
+        torch.manual_seed(100 + k)
+        np.random.seed(100 + k)
+        C = getattr(mods[modkey], cls)
+        with contextlib.redirect_stdout(io.StringIO()):
+            if modkey == "deep":
+                obj = C(Xi, 1.0, M, N, D, layers, mode, act)
+            else:
+                obj = C(Xi, 1.0, M, N, D, Mm, layers, mode, act)
+        p0 = _flat(obj.model.state_dict())
+        np.random.seed(200 + k)
+        with contextlib.redirect_stdout(io.StringIO()):
+            obj.train(iters, lr)
+        p1 = _flat(obj.model.state_dict())
+        np.savez_compressed(os.path.join(OUT, f"g1_{name}.npz"), name=name, problem=prob, mode=mode,
+                            activation=act, layers=np.array(layers), Xi=Xi.astype(np.float32), M=M, N=N,
+                            T=1.0, Mm=-1.0 if Mm is None else Mm, iters=iters, lr=lr, batch_seed=200 + k,
+                            clip=modkey != "deep", params0=p0, params1=p1)
+        print(f"{name:42s} |dp|={np.abs(p1 - p0).max():.3e}")
+
+
+def north_star(mods, seed=0, steps=(1, 3)):
+    """G2: D=100, layers [101,110x4,1] NAIS-Net Sine BSB, M=1024, N=50."""
+    import torch
+    D, M, N = 100, 1024, 50
+    layers = [D + 1] + 4 * [110] + [1]
+    Xi = np.array([1.0, 0.5] * (D // 2))[None, :]
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    with contextlib.redirect_stdout(io.StringIO()):
+        obj = mods["deep"].BlackScholesBarenblatt(Xi, 1.0, M, N, D, layers, "NAIS-Net", "Sine")
+    p0 = _flat(obj.model.state_dict())
+    np.random.seed(1000 + seed)          # batch recipe: legacy MT19937 stream, seed 1000+seed
+    res = _run_case(obj, M, N, D, full_z=False)
+    out = dict(name="north_star", problem="bsb", mode="NAIS-Net", activation="Sine",
+               layers=np.array(layers), Xi=Xi.astype(np.float32), M=M, N=N, T=1.0, seed=seed,
+               batch_seed=1000 + seed, params=p0, loss=res["loss"], Y=res["Y"], grad=res["grad"],
+               used=res["used"], X_sum=np.float64(res["X"].astype(np.float64).sum()),
+               X_sumsq=np.float64((res["X"].astype(np.float64) ** 2).sum()), X_first=res["X"][:2])
+    # reference train(): Adam, lr 1e-3, no clip, starting again from the same batch seed
+    np.random.seed(1000 + seed)
+    done = 0
+    for s in steps:
+        with contextlib.redirect_stdout(io.StringIO()):
+            obj.train(s - done, 1e-3)
+        done = s
+        out[f"params_after_{s}"] = _flat(obj.model.state_dict())
+    np.savez_compressed(os.path.join(OUT, "g2_north_star.npz"), **out)
+    print(f"north_star loss={res['loss']:.6e} Y0={res['Y'][0, 0, 0]:.6f}")
+
+
+if __name__ == "__main__":
+    m = _setup()
+    small_cases(m)
+    train_cases(m)
+    if "--skip-north-star" not in sys.argv:
+        north_star(m)

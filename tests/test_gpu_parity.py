@@ -1,0 +1,187 @@
+"""HIP path (through the C ABI) vs the reference's golden vectors and the
+oracle.  Needs an MI355X.
+
+Tolerances (fp32 arithmetic; the HIP GEMMs sum in a different order than
+the reference's CPU BLAS):
+  X (Euler-Maruyama rollout)    bit-exact (same op order, no contraction)
+  loss                          rel 1e-4
+  Y, Z                          abs 1e-4 * max(1, |ref|max)
+  gradient                      abs 2e-4 * max|ref grad|
+  parameters after 10 Adam steps abs 5e-5 ; north-star Y0 after 1/3 steps |dY0| < 1e-3
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_pkg
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+G1 = sorted(p for p in glob.glob(os.path.join(GOLDEN, "g1_*.npz")) if "train_" not in p)
+
+
+def _load(p):
+    z = np.load(p)
+    return {k: z[k] for k in z.files}
+
+
+def spec_for(pkg, problem, D):
+    S = pkg.ProblemSpec
+    return {
+        "bsb": S(sig_a=0.4, phi_r=0.05, phi_c=1.0, g="sumsq"),
+        "bspde_test": S(mu_a=0.05, sig_a=0.2, phi_r=0.05, phi_c=1.0, g="sumsq"),
+        "call": S(mu_a=0.05, sig_a=0.2, phi_r=0.05, phi_c=1.0, g="call_sum", strike=1.0 * D),
+        "call1d": S(mu_a=0.01, sig_a=0.25, phi_r=0.01, phi_c=0.0, g="call_sum", strike=1.0 * D),
+        "basket": S(mu_a=0.05, sig_a=0.2, phi_r=0.05, phi_c=0.0, g="call_mean", strike=1.0),
+        "hjb": S(sig_b=float(np.sqrt(2.0)), phi_zz=1.0, g="log"),
+    }[problem]
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    return load_pkg()
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU test run without a GPU"
+    return torch.device("cuda:0")
+
+
+def native_case(pkg, dev, g, want_grad=True):
+    layers = [int(v) for v in g["layers"]]
+    D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
+    s = pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]), spec_for(pkg, str(g["problem"]), D),
+                         float(g["T"]), dev)
+    params = torch.from_numpy(g["params"]).to(dev)
+    out = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (N + 1) * D, device=dev),
+               Y=torch.empty(M * (N + 1), device=dev), Z=torch.empty(M * (N + 1) * D, device=dev))
+    grad = torch.empty_like(params) if want_grad else None
+    s.loss_grad(params, M, N, torch.from_numpy(g["Xi"]).to(dev).contiguous(),
+                t=torch.from_numpy(g["t"]).to(dev).reshape(M, N + 1).contiguous(),
+                W=torch.from_numpy(g["W"]).to(dev).contiguous(), grad=grad, **out)
+    torch.cuda.synchronize()
+    res = {k: v.cpu().numpy() for k, v in out.items()}
+    res["X"] = res["X"].reshape(M, N + 1, D)
+    res["Z"] = res["Z"].reshape(M, N + 1, D)
+    res["Y"] = res["Y"].reshape(M, N + 1, 1)
+    if want_grad:
+        res["grad"] = grad.cpu().numpy()
+    return res
+
+
+@pytest.mark.parametrize("path", G1, ids=[os.path.basename(p)[3:-4] for p in G1])
+def test_loss_grad_matches_reference(pkg, dev, path):
+    g = _load(path)
+    r = native_case(pkg, dev, g)
+    np.testing.assert_array_equal(r["X"], g["X"])
+    np.testing.assert_allclose(r["loss"][0], g["loss"], rtol=1e-4)
+    np.testing.assert_allclose(r["Y"], g["Y"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Y"]).max()))
+    np.testing.assert_allclose(r["Z"], g["Z"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Z"]).max()))
+    used = g["used"]
+    assert np.all(r["grad"][~used] == 0)
+    np.testing.assert_allclose(r["grad"][used], g["grad"][used], rtol=0, atol=2e-4 * np.abs(g["grad"]).max())
+
+
+@pytest.mark.parametrize("path", G1[:3], ids=[os.path.basename(p)[3:-4] for p in G1[:3]])
+def test_forward_only_matches(pkg, dev, path):
+    g = _load(path)
+    r = native_case(pkg, dev, g, want_grad=False)
+    np.testing.assert_allclose(r["loss"][0], g["loss"], rtol=1e-4)
+
+
+def test_repeatable(pkg, dev):
+    g = _load(G1[0])
+    a = native_case(pkg, dev, g)
+    b = native_case(pkg, dev, g)
+    np.testing.assert_array_equal(a["grad"], b["grad"])     # deterministic reductions (no atomics)
+    np.testing.assert_array_equal(a["loss"], b["loss"])
+
+
+def test_train_deepbsde_surface_matches_reference(pkg, dev):
+    """DeepBSDE.FBSNN.train (Adam, no clip) for 10 iterations from the same
+    params and numpy stream as the reference."""
+    g = _load(os.path.join(GOLDEN, "g1_train_deep_bsb_NAIS-Net_Sine.npz"))
+    layers = [int(v) for v in g["layers"]]
+    D = layers[0] - 1
+    m = pkg.BlackScholesBarenblatt(g["Xi"], float(g["T"]), int(g["M"]), int(g["N"]), D, layers,
+                                   str(g["mode"]), str(g["activation"]), device=dev)
+    m.params.copy_(torch.from_numpy(g["params0"]).to(dev))
+    np.random.seed(int(g["batch_seed"]))
+    graph = m.train(int(g["iters"]), float(g["lr"]))
+    assert graph.shape[0] == 2
+    np.testing.assert_allclose(m.params.cpu().numpy(), g["params1"], rtol=0, atol=5e-5)
+
+
+def test_train_nd_surface_matches_reference(pkg, dev):
+    """nd_BSPDE_case.FBSNN.train (Mm schedule, clip 1.0, Adam)."""
+    g = _load(os.path.join(GOLDEN, "g1_train_nd_call_Naisnet_Sine.npz"))
+    layers = [int(v) for v in g["layers"]]
+    D = layers[0] - 1
+    m = pkg.CallOption(g["Xi"], float(g["T"]), int(g["M"]), int(g["N"]), D, float(g["Mm"]), layers,
+                       str(g["mode"]), str(g["activation"]), device=dev)
+    m.params.copy_(torch.from_numpy(g["params0"]).to(dev))
+    np.random.seed(int(g["batch_seed"]))
+    graph, min_loss, state = m.train(int(g["iters"]), float(g["lr"]))
+    assert np.isfinite(min_loss) and state[0].shape[1] == int(g["N"]) + 1
+    np.testing.assert_allclose(m.params.cpu().numpy(), g["params1"], rtol=0, atol=5e-5)
+
+
+def test_north_star_shape(pkg, dev):
+    """G2: 100-D BSB, NAIS-Net [101,110x4,1], M=1024, N=50, from the
+    reference's own init and numpy stream; Y0 after 1 and 3 Adam steps."""
+    g = _load(os.path.join(GOLDEN, "g2_north_star.npz"))
+    layers = [int(v) for v in g["layers"]]
+    D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
+    m = pkg.BlackScholesBarenblatt(g["Xi"], float(g["T"]), M, N, D, layers, "NAIS-Net", "Sine", device=dev)
+    m.params.copy_(torch.from_numpy(g["params"]).to(dev))
+    np.random.seed(int(g["batch_seed"]))
+    t, W = m.fetch_minibatch()
+    out = m._run(t, W, m.Xi, grad=m.grad)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(float(out["loss"]), float(g["loss"]), rtol=1e-4)
+    np.testing.assert_allclose(out["Y"].cpu().numpy(), g["Y"], rtol=0, atol=1e-3)
+    X = out["X"].cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(X.sum(), float(g["X_sum"]), rtol=1e-12)
+    np.testing.assert_array_equal(out["X"][:2].cpu().numpy(), g["X_first"])
+    used = g["used"]
+    gr = m.grad.cpu().numpy()
+    np.testing.assert_allclose(gr[used], g["grad"][used], rtol=0, atol=2e-4 * np.abs(g["grad"]).max())
+    # training: reference train() from the same batch seed
+    m.params.copy_(torch.from_numpy(g["params"]).to(dev))
+    np.random.seed(int(g["batch_seed"]))
+    done = 0
+    for s in (1, 3):
+        m.train(s - done, 1e-3)
+        done = s
+        ref = g[f"params_after_{s}"]
+        np.testing.assert_allclose(m.params.cpu().numpy(), ref, rtol=0, atol=2e-5 * s)
+    # Y0 = u(0, X0) of the trained parameters
+    m2_params = torch.from_numpy(g["params_after_3"]).to(dev)
+    t0 = torch.zeros(1, device=dev)
+    x0 = torch.from_numpy(g["Xi"]).to(dev).reshape(1, D)
+    u_nat, _ = m.net_u(t0, x0)
+    m.params.copy_(m2_params)
+    u_ref_params, _ = m.net_u(t0, x0)
+    assert abs(float(u_nat) - float(u_ref_params)) < 1e-3
+
+
+def test_net_u_matches_fixture_Y(pkg, dev):
+    g = _load(G1[0])
+    layers = [int(v) for v in g["layers"]]
+    D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
+    s = pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]), spec_for(pkg, str(g["problem"]), D),
+                         float(g["T"]), dev)
+    params = torch.from_numpy(g["params"]).to(dev)
+    R = M * (N + 1)
+    t = torch.from_numpy(g["t"]).to(dev).reshape(R).contiguous()
+    X = torch.from_numpy(g["X"]).to(dev).reshape(R, D).contiguous()
+    u = torch.empty(R, device=dev)
+    du = torch.empty(R, D, device=dev)
+    s.net_u(params, t, X, u, du)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(u.cpu().numpy(), g["Y"].reshape(R), rtol=0, atol=1e-4)
+    np.testing.assert_allclose(du.cpu().numpy(), g["Z"].reshape(R, D), rtol=0, atol=1e-4)
