@@ -30,7 +30,6 @@ namespace {
 thread_local std::string g_last_error;
 
 constexpr int TN_SPLITS = 32;   // fixed split count -> static slab layout
-constexpr int OUT_SPLITS = 64;  // output-layer column-sum splits
 
 inline int pad16(int x) { return (x + 15) / 16 * 16; }
 inline int padw(int x) { return x <= 128 ? pad16(x) : (x + 127) / 128 * 128; }
@@ -81,6 +80,8 @@ struct dbsde_ctx {
   long long* d_woffs = nullptr;   // NAIS: W_j offsets in the flat params
   float** d_rtr = nullptr;
   float** d_abar = nullptr;
+  float** d_sbuf = nullptr;
+  double* proj_part = nullptr;
   unsigned char* d_used = nullptr;
   PackDesc* d_prep = nullptr;
   int n_prep = 0;
@@ -88,8 +89,6 @@ struct dbsde_ctx {
   int n_fin = 0;
   std::vector<float*> slab;  // TN problem slabs (0 = x-stack, j = block j)
   std::vector<int> slab_mt, slab_nt;
-  float* out_slab = nullptr;
-  int out_ld = 0;
   double* opt_part = nullptr;
   int opt_nparts = 0;
 
@@ -100,6 +99,7 @@ struct dbsde_ctx {
         *G = nullptr;
   float* Pbuf[2] = {nullptr, nullptr};
   float *u = nullptr, *rres = nullptr, *lossrow = nullptr, *ubar = nullptr, *q3S = nullptr;
+  float *u16 = nullptr, *o16 = nullptr;  // [Rp,16]: col 0 = ubar / 1 (output-layer TN operands)
   double* loss_part = nullptr;
   float* loss_tmp = nullptr;
 
@@ -202,6 +202,7 @@ int build_net(dbsde_ctx* c) {
   if (c->L.back() != 1) return fail(c, DBSDE_EINVAL, "last layer width must be 1 (u is a scalar)");
   if (c->D < 1) return fail(c, DBSDE_EINVAL, "layers[0] must be D+1 >= 2");
   c->K = n - 3;
+  if (c->K > 6) return fail(c, DBSDE_EINVAL, "at most 6 hidden blocks (len(layers) <= 9) are supported");
   c->mode = g.mode;
   c->act = g.activation;
   if (c->act < 0 || c->act > 2) return fail(c, DBSDE_EINVAL, "unknown activation");
@@ -323,17 +324,21 @@ int build_buffers(dbsde_ctx* c) {
   const int LW = c->L[1];
   if (c->proj) {
     if ((rc = dalloc_t(c, &c->norms, (size_t)K + 1))) return rc;
-    std::vector<float*> hr(K), ha(K);
+    std::vector<float*> hr(K), ha(K), hs(K);
     std::vector<long long> hw(K);
     for (int j = 1; j <= K; ++j) {
       if ((rc = dalloc_t(c, &c->rtr[j], (size_t)LW * LW))) return rc;
       if ((rc = dalloc_t(c, &c->abar[j], (size_t)LW * LW))) return rc;
+      if ((rc = dalloc_t(c, &hs[j - 1], (size_t)LW * LW))) return rc;
       hr[j - 1] = c->rtr[j];
       ha[j - 1] = c->abar[j];
       hw[j - 1] = c->B[j - 1].w;
     }
+    if ((rc = dalloc_t(c, &c->proj_part, (size_t)K * ((LW * LW + 255) / 256)))) return rc;
     if ((rc = dalloc_t(c, &c->d_rtr, K))) return rc;
     if ((rc = dalloc_t(c, &c->d_abar, K))) return rc;
+    if ((rc = dalloc_t(c, &c->d_sbuf, K))) return rc;
+    HIPC(c, hipMemcpy(c->d_sbuf, hs.data(), K * sizeof(float*), hipMemcpyHostToDevice));
     if ((rc = dalloc_t(c, &c->d_woffs, K))) return rc;
     HIPC(c, hipMemcpy(c->d_rtr, hr.data(), K * sizeof(float*), hipMemcpyHostToDevice));
     HIPC(c, hipMemcpy(c->d_abar, ha.data(), K * sizeof(float*), hipMemcpyHostToDevice));
@@ -390,11 +395,13 @@ int build_buffers(dbsde_ctx* c) {
     c->slab_nt[j] = (n + 63) / 64;
     return dalloc_t(c, &c->slab[j], (size_t)TN_SPLITS * c->slab_mt[j] * 64 * c->slab_nt[j] * 64);
   };
+  c->slab.resize(K + 2, nullptr);
+  c->slab_mt.resize(K + 2, 0);
+  c->slab_nt.resize(K + 2, 0);
   if ((rc = mkslab(0, c->Stot_x, Dp))) return rc;
   for (int j = 1; j <= K; ++j)
     if ((rc = mkslab(j, c->Wp[j], c->Wp[j - 1] + (c->has_v ? 0 : 1)))) return rc;
-  c->out_ld = c->L[c->K + 1] + 1;
-  if ((rc = dalloc_t(c, &c->out_slab, (size_t)OUT_SPLITS * c->out_ld))) return rc;
+  if ((rc = mkslab(K + 1, 16, c->Wp[K] + 1))) return rc;  // output layer: [w_out | b_out]
 
   std::vector<PackDesc> F;
   auto slabsum = [&](int j, int r0, int c0, int rows, int cols, float* dst, int dst_ld, float scale) {
@@ -422,16 +429,8 @@ int build_buffers(dbsde_ctx* c) {
       slabsum(j, 0, c->Wp[j - 1], b.out, 1, gtag(b.b), 1, 1.f);
     }
   }
-  {
-    PackDesc d = mk_desc(c->out_slab, c->out_ld, gtag(c->out.w), 1, 1, c->L[c->K + 1], 0, PK_SLABSUM);
-    d.nslab = OUT_SPLITS;
-    d.slab_stride = c->out_ld;
-    F.push_back(d);
-    d = mk_desc(c->out_slab + c->L[c->K + 1], c->out_ld, gtag(c->out.b), 1, 1, 1, 0, PK_SLABSUM);
-    d.nslab = OUT_SPLITS;
-    d.slab_stride = c->out_ld;
-    F.push_back(d);
-  }
+  slabsum(K + 1, 0, 0, 1, c->out.in, gtag(c->out.w), 1, 1.f);
+  slabsum(K + 1, 0, c->Wp[K], 1, 1, gtag(c->out.b), 1, 1.f);
   c->n_fin = (int)F.size();
   if ((rc = dalloc_t(c, &c->d_prep, P.size()))) return rc;
   if ((rc = dalloc_t(c, &c->d_fin, F.size()))) return rc;
@@ -474,6 +473,10 @@ int ensure_rows(dbsde_ctx* c, int Rp, int N) {
   if ((rc = dalloc_t(c, &c->rres, R))) return rc;
   if ((rc = dalloc_t(c, &c->lossrow, R))) return rc;
   if ((rc = dalloc_t(c, &c->ubar, R))) return rc;
+  if ((rc = dalloc_t(c, &c->u16, R * 16))) return rc;
+  if ((rc = dalloc_t(c, &c->o16, R * 16))) return rc;
+  fill_col0_kernel<<<(unsigned)((R + 255) / 256), 256, 0, c->stream>>>(c->o16, 16, (long long)R, 1.f);
+  HIPC(c, hipGetLastError());
   if ((rc = dalloc_t(c, &c->loss_part, R / 256 + 2))) return rc;
   if ((rc = dalloc_t(c, &c->loss_tmp, 16))) return rc;
   if ((rc = dalloc_t(c, &c->q3S, (size_t)nn + 1))) return rc;
@@ -564,62 +567,84 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
       d.dst[(size_t)r * d.dst_ld + cc] = v;
   }
 }
+// RtR_j = W_j^T W_j (Functions/naisnet.py:33), one thread per element, and
+// per-block partial sums of squares for the Frobenius norm (fixed order).
 __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, const long long* woffs, int L,
-                                                         float* const* rtr, int ldr, double* norms) {
-  const int j = blockIdx.x;
+                                                         float* const* rtr, double* part, int nblk) {
+  const int j = blockIdx.y;
   const float* W = params + woffs[j];
-  float* R = rtr[j];
-  __shared__ double red[256];
+  const int i = blockIdx.x * 256 + threadIdx.x;
   double sq = 0.0;
-  for (int i = threadIdx.x; i < L * L; i += 256) {
+  if (i < L * L) {
     const int a = i / L, b = i - a * L;
     float s = 0.f;
     for (int k = 0; k < L; ++k) s += W[k * L + a] * W[k * L + b];
-    R[a * ldr + b] = s;
-    sq += (double)s * (double)s;
+    rtr[j][i] = s;
+    sq = (double)s * (double)s;
   }
+  __shared__ double red[256];
   red[threadIdx.x] = sq;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) norms[j] = sqrt(red[0]);
+  if (threadIdx.x == 0) part[j * nblk + blockIdx.x] = red[0];
 }
-// Q4 adjoint; W from params, Wbar into grad.
-__global__ void __launch_bounds__(256) proj_adjoint_params_kernel(const float* params, const long long* woffs,
-                                                                  float* const* rtr, float* const* abar,
-                                                                  const double* norms, int L, float* grad) {
+// norms[j] = sqrt(sum of partials) ; thread j (deterministic order)
+__global__ void norm_from_parts_kernel(const double* part, int nblk, int K, double* norms) {
+  const int j = threadIdx.x;
+  if (j >= K) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += part[j * nblk + b];
+  norms[j] = sqrt(s);
+}
+// <Abar_j, R_j> partial sums per block
+__global__ void __launch_bounds__(256) proj_dot_kernel(float* const* abar, float* const* rtr, int L, double* part,
+                                                       int nblk) {
   const int j = blockIdx.y;
-  const float* W = params + woffs[j];
-  const float* R = rtr[j];
-  const float* Ab = abar[j];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  double d = 0.0;
+  if (i < L * L) d = (double)abar[j][i] * (double)rtr[j][i];
   __shared__ double red[256];
-  double dot = 0.0;
-  for (int i = threadIdx.x; i < L * L; i += 256) dot += (double)Ab[i] * (double)R[i];
-  red[threadIdx.x] = dot;
+  red[threadIdx.x] = d;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  dot = red[0];
+  if (threadIdx.x == 0) part[j * nblk + blockIdx.x] = red[0];
+}
+// S = Rbar + Rbar^T with Rbar = c n^-1/2 (Abar - 1/2 <Abar,R> R / n^2) if the
+// Q4 branch was taken, else Abar.  Written over abar's scratch twin sbuf.
+__global__ void __launch_bounds__(256) proj_s_kernel(float* const* abar, float* const* rtr, float* const* sbuf, int L,
+                                                     const double* part, int nblk, const double* norms) {
+  const int j = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L * L) return;
+  double dot = 0.0;
+  for (int b = 0; b < nblk; ++b) dot += part[j * nblk + b];
   const double n = norms[j];
   const bool taken = (float)n > 0.98f;
   const float cA = taken ? (float)(0.98994949366116658 / sqrt(n)) : 1.f;
   const float cR = taken ? (float)(0.98994949366116658 / sqrt(n) * 0.5 * dot / (n * n)) : 0.f;
-  float* Wb = grad + woffs[j];
-  const int rows0 = blockIdx.x * 8;
-  for (int i = threadIdx.x; i < 8 * L; i += 256) {
-    const int a = rows0 + i / L, b = i % L;
-    if (a >= L) continue;
-    float s = 0.f;
-    for (int k = 0; k < L; ++k) {
-      const float Sv = cA * (Ab[k * L + b] + Ab[b * L + k]) - cR * (R[k * L + b] + R[b * L + k]);
-      s += W[a * L + k] * Sv;
-    }
-    Wb[a * L + b] = s;
-  }
+  const int a = i / L, b = i - a * L;
+  const float* Ab = abar[j];
+  const float* R = rtr[j];
+  sbuf[j][i] = cA * (Ab[a * L + b] + Ab[b * L + a]) - cR * (R[a * L + b] + R[b * L + a]);
+}
+// Wbar_j = W_j S_j  -> grad (one thread per element)
+__global__ void __launch_bounds__(256) proj_wbar_kernel(const float* params, const long long* woffs,
+                                                        float* const* sbuf, int L, float* grad) {
+  const int j = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= L * L) return;
+  const int a = i / L, b = i - a * L;
+  const float* W = params + woffs[j];
+  const float* S = sbuf[j];
+  float s = 0.f;
+  for (int k = 0; k < L; ++k) s += W[a * L + k] * S[k * L + b];
+  grad[woffs[j] + i] = s;
 }
 }  // namespace dbsde
 
@@ -630,7 +655,10 @@ int prep_weights(dbsde_ctx* c, const float* params) {
   const int LW = c->L[1];
   if (c->proj) {
     const double fl = 2.0 * c->K * LW * (double)LW * LW;
-    RUN(c, "rtr", fl, 0.0, rtr_params_kernel<<<c->K, 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, LW, c->norms));
+    const int nblk = (LW * LW + 255) / 256;
+    RUN(c, "rtr", fl, 0.0,
+        rtr_params_kernel<<<dim3(nblk, c->K), 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, c->proj_part, nblk));
+    RUN(c, "rtr_norm", 0.0, 0.0, norm_from_parts_kernel<<<1, 64, 0, s>>>(c->proj_part, nblk, c->K, c->norms));
   }
   RUN(c, "pack_weights", 0.0, 0.0, pack_tagged_kernel<<<dim3(8, c->n_prep), 256, 0, s>>>(c->d_prep, params, nullptr));
   return DBSDE_OK;
@@ -641,10 +669,13 @@ int finalize_grads(dbsde_ctx* c, const float* params, float* grad) {
   RUN(c, "grad_finalize", 0.0, 0.0, pack_tagged_kernel<<<dim3(16, c->n_fin), 256, 0, s>>>(c->d_fin, params, grad));
   if (c->proj) {
     const int LW = c->L[1];
-    const double fl = 2.0 * c->K * LW * (double)LW * LW;
-    RUN(c, "proj_adjoint", fl, 0.0,
-        proj_adjoint_params_kernel<<<dim3((LW + 7) / 8, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_rtr, c->d_abar,
-                                                                            c->norms, LW, grad));
+    const int nblk = (LW * LW + 255) / 256;
+    const dim3 g(nblk, c->K);
+    RUN(c, "proj_dot", 0.0, 0.0, proj_dot_kernel<<<g, 256, 0, s>>>(c->d_abar, c->d_rtr, LW, c->proj_part, nblk));
+    RUN(c, "proj_s", 0.0, 0.0,
+        proj_s_kernel<<<g, 256, 0, s>>>(c->d_abar, c->d_rtr, c->d_sbuf, LW, c->proj_part, nblk, c->norms));
+    RUN(c, "proj_wbar", 2.0 * c->K * LW * (double)LW * LW, 0.0,
+        proj_wbar_kernel<<<g, 256, 0, s>>>(params, c->d_woffs, c->d_sbuf, LW, grad));
   }
   return DBSDE_OK;
 }
@@ -889,7 +920,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   }
   RUN(c, "ubar_loss", 0.0, 16.0 * R,
       ubar_kernel<<<Rp / 256 + 1, 256, 0, s>>>(c->rres, c->xin, c->Dp, R, Rp, N1, pr.phi_r, c->lossrow, c->ubar,
-                                               c->loss_part));
+                                               c->u16, c->loss_part));
   float* loss_dst = (out && out->loss) ? out->loss : c->loss_tmp;
   RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, s>>>(c->loss_part, Rp / 256 + 1, loss_dst));
 
@@ -1021,12 +1052,31 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
       maxt = std::max(maxt, pj.mt * pj.nt);
       tfl += 2.0 * 2.0 * R * L[j] * (L[j + 1] + (c->has_v ? 0 : 1));
     }
-    if (K + 1 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
-    RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, TN_SPLITS, K + 1), 256, 0, s>>>(ta));
-    const int orps = (Rp + OUT_SPLITS - 1) / OUT_SPLITS;
-    RUN(c, "out_layer_grad", 4.0 * R * L[K + 1], 8.0 * R * L[K + 1],
-        outgrad_kernel<<<OUT_SPLITS, 256, 0, s>>>(c->ubar, c->H + c->col[K], c->Hdot + c->col[K], S, L[K + 1], orps,
-                                                  Rp, c->out_ld, c->out_slab));
+    {
+      // output layer: [w_out | b_out] = sum_r ubar_r [h_{K+1} | 1] + hdot_{K+1}
+      TNProb& po = ta.prob[K + 1];
+      po.A[0] = c->u16;
+      po.lda[0] = 16;
+      po.nA[0] = 16;
+      po.B[0] = c->H + c->col[K];
+      po.ldb[0] = S;
+      po.nB[0] = c->Wp[K];
+      po.A[1] = c->o16;
+      po.lda[1] = 16;
+      po.nA[1] = 16;
+      po.B[1] = c->Hdot + c->col[K];
+      po.ldb[1] = S;
+      po.nB[1] = c->Wp[K];
+      po.npairs = 2;
+      po.ones_col = c->Wp[K];
+      po.mt = c->slab_mt[K + 1];
+      po.nt = c->slab_nt[K + 1];
+      po.slab = c->slab[K + 1];
+      maxt = std::max(maxt, po.mt * po.nt);
+      tfl += 2.0 * 2.0 * R * (L[K + 1] + 1);
+    }
+    if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
+    RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, TN_SPLITS, K + 2), 256, 0, s>>>(ta));
     if ((rc = finalize_grads(c, params, grad))) return rc;
   }
 

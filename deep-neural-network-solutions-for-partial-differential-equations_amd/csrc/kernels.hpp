@@ -456,7 +456,7 @@ __global__ void __launch_bounds__(256) rowdot_kernel(const float* H, int ldh, in
 // rres[r] = Y_{n+1} - Ytilde_{n+1} (n < N), or Y_N - g(X_N) (n == N).
 __global__ void __launch_bounds__(256) ubar_kernel(const float* rres, const float* xin, int ldx, int R, int Rp,
                                                    int N1, float phi_r, const float* lossrow, float* ubar,
-                                                   double* loss_part) {
+                                                   float* u16, double* loss_part) {
   const int row = blockIdx.x * 256 + threadIdx.x;
   float ub = 0.f;
   double lv = 0.0;
@@ -471,7 +471,10 @@ __global__ void __launch_bounds__(256) ubar_kernel(const float* rres, const floa
     }
     lv = (double)lossrow[row];
   }
-  if (row < Rp) ubar[row] = ub;
+  if (row < Rp) {
+    ubar[row] = ub;
+    u16[(size_t)row * 16] = ub;
+  }
   __shared__ double red[256];
   red[threadIdx.x] = lv;
   __syncthreads();
@@ -597,24 +600,9 @@ __global__ void __launch_bounds__(256) tn_gemm_kernel(TNArgs args) {
       }
 }
 
-// column sums for the output layer: slab[s][c] = sum_r ubar[r]*H[r,c] + Hd[r,c]
-// (c < ncols), slab[s][ncols] = sum_r ubar[r]
-__global__ void __launch_bounds__(256) outgrad_kernel(const float* ubar, const float* H, const float* Hd, int ldh,
-                                                      int ncols, int rows_per_split, int Rp, int ldslab,
-                                                      float* slab) {
-  const int split = blockIdx.x;
-  const int r0 = split * rows_per_split;
-  int r1 = r0 + rows_per_split;
-  if (r1 > Rp) r1 = Rp;
-  for (int c = threadIdx.x; c <= ncols; c += 256) {
-    float s = 0.f;
-    if (c < ncols) {
-      for (int r = r0; r < r1; ++r) s += ubar[r] * H[(size_t)r * ldh + c] + Hd[(size_t)r * ldh + c];
-    } else {
-      for (int r = r0; r < r1; ++r) s += ubar[r];
-    }
-    slab[(size_t)split * ldslab + c] = s;
-  }
+__global__ void __launch_bounds__(256) fill_col0_kernel(float* buf, int ld, long long rows, float v) {
+  const long long r = blockIdx.x * 256LL + threadIdx.x;
+  if (r < rows) buf[r * ld] = v;
 }
 
 // --------------------------------------------------------------------------

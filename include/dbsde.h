@@ -76,7 +76,7 @@ typedef struct dbsde_problem {
 typedef struct dbsde_config {
   int mode;          /* DBSDE_MODE_*                                   */
   int activation;    /* DBSDE_ACT_*                                    */
-  int n_layers;      /* len(layers), 3..16                             */
+  int n_layers;      /* len(layers), 4..9                              */
   int layers[16];    /* [D+1, W1, ..., Wk, 1]                          */
   dbsde_problem problem;
   float T;           /* terminal time                                  */

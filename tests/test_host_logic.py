@@ -1,0 +1,118 @@
+"""Host-side logic of the package against the oracle and the reference's
+golden vectors (layouts, initialisation, problem coefficients, schedule).  CPU."""
+import glob
+import os
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, load_pkg
+from oracle import fbsnn_ref as fr
+from oracle import timeparallel as tp
+
+G1 = sorted(p for p in glob.glob(os.path.join(GOLDEN, "g1_*.npz")) if "train_" not in p)
+MODES = ["FC", "NAIS-Net", "Resnet", "Naisnet"]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("layers", [[5, 16, 16, 16, 16, 1], [101, 110, 110, 110, 110, 1], [2, 8, 8, 1],
+                                    [5, 16, 16, 16, 1]])
+def test_param_layout_matches_reference_modules(mode, layers):
+    from importlib import import_module
+    nets = import_module(load_pkg().__name__ + ".networks")
+    m = nets.make_model(mode, layers, "Sine")
+    got = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    assert got == [(k, tuple(s)) for k, s in tp.param_layout(mode, layers)]
+    ref = fr.build_model(mode, layers, "Sine")
+    assert [k for k in ref.state_dict()] == [k for k, _ in got]
+
+
+@pytest.mark.parametrize("path", G1, ids=[os.path.basename(p)[3:-4] for p in G1])
+def test_initialisation_reproduces_reference(path):
+    """torch.manual_seed(s) + the package's model builder == the reference's
+    own construction (the fixture's params were drawn by the reference)."""
+    from importlib import import_module
+    nets = import_module(load_pkg().__name__ + ".networks")
+    z = np.load(path)
+    torch.manual_seed(int(z["seed"]))
+    m = nets.make_model(str(z["mode"]), [int(v) for v in z["layers"]], str(z["activation"]))
+    flat = torch.cat([p.reshape(-1) for p in m.state_dict().values()]).numpy()
+    np.testing.assert_array_equal(flat, z["params"])
+
+
+def test_problem_specs_match_oracle_table():
+    pkg = load_pkg()
+    ns = types.SimpleNamespace(strike=4.0, D=4)
+    cases = {"call": pkg.CallOption, "call1d": pkg.CallOption1D, "basket": pkg.BasketCallOption,
+             "bspde_test": pkg.BSPDETestCase, "hjb": pkg.HamiltonJacobiBellman, "bsb": pkg.BlackScholesBarenblatt}
+    g_map = {"sumsq": "sumsq", "call_sum": "call_sum", "call_mean": "call_mean", "log": "log"}
+    for kind, cls in cases.items():
+        spec = cls.problem_spec(ns)
+        mu_a, sig_a, sig_b, phi_r, phi_c, phi_zz, gk = tp.PROBLEMS[kind]
+        assert np.allclose([spec.mu_a, spec.sig_a, spec.sig_b, spec.phi_r, spec.phi_c, spec.phi_zz],
+                           [mu_a, sig_a, sig_b, phi_r, phi_c, phi_zz]), kind
+        assert g_map[spec.g] == gk, kind
+
+
+def test_problem_torch_expressions_match_oracle():
+    """phi_tf/g_tf/mu_tf/sigma_tf of the package classes == the reference's (via the oracle)."""
+    pkg = load_pkg()
+    D = 4
+    torch.manual_seed(0)
+    X, Z, Y, t = torch.rand(3, D) + 0.5, torch.randn(3, D), torch.randn(3, 1), torch.zeros(3, 1)
+    for kind, cls in {"call": pkg.CallOption, "basket": pkg.BasketCallOption, "hjb": pkg.HamiltonJacobiBellman,
+                      "bsb": pkg.BlackScholesBarenblatt, "bspde_test": pkg.BSPDETestCase}.items():
+        ref = fr.make_problem(kind, D)
+        self = types.SimpleNamespace(strike=ref.strike, D=D)
+        self_cls = type("S", (cls,), {})
+        obj = object.__new__(self_cls)
+        obj.__dict__.update(self.__dict__)
+        assert torch.allclose(obj.phi_tf(t, X, Y, Z), ref.phi(t, X, Y, Z)), kind
+        assert torch.allclose(obj.g_tf(X), ref.g(X)), kind
+        assert torch.allclose(obj.mu_tf(t, X, Y, Z), ref.mu(t, X, Y, Z)), kind
+        assert torch.allclose(obj.sigma_tf(t, X, Y), ref.sigma(t, X, Y)), kind
+
+
+@pytest.mark.parametrize("schedule,Mm", [("nd", 50 ** (1 / 5)), ("nd", 5.0)])
+def test_n_schedule(schedule, Mm):
+    pkg = load_pkg()
+    obj = object.__new__(pkg.CallOption)
+    obj.schedule, obj.Mm, obj.N = schedule, Mm, 50
+    for it in (0, 100, 3999, 4000, 8000, 12000, 16000, 19999):
+        obj._schedule_n(it)
+        assert obj.N == fr.n_schedule(it, Mm, 50), it
+
+
+def test_corr_schedule_collapses_like_reference():
+    """with_corr...:406-409 re-applies N**(1/5) to the mutated N."""
+    pkg = load_pkg()
+    obj = object.__new__(pkg.BasketCallOption)
+    obj.schedule, obj.Mm, obj.N = "corr", 50 ** (1 / 5), 200
+    seq = []
+    for it in range(4):
+        obj._schedule_n(it)
+        seq.append(obj.N)
+    assert seq == [3, 2, 2, 2]
+
+
+def test_correlation_matrix_recipe_matches_reference_fixture():
+    """generate_correlation_matrix (Q10) reproduces the reference's matrix from
+    the same numpy stream (fixture drawn by the reference constructor)."""
+    pkg = load_pkg()
+    z = np.load(os.path.join(GOLDEN, "g1_corr_basket_Naisnet_ReLU.npz"))
+    np.random.seed(int(z["seed"]))
+    obj = object.__new__(pkg.BasketCallOption)
+    obj.correlation_type = "random_correlation"
+    np.testing.assert_allclose(obj.generate_correlation_matrix(4), z["corr"], rtol=0, atol=1e-12)
+
+
+def test_optimizer_names():
+    pkg = load_pkg()
+    obj = object.__new__(pkg.CallOption)
+    with pytest.raises(ValueError):
+        obj._check_optimizer("Nadam")
+    with pytest.raises(NotImplementedError):
+        obj._check_optimizer("LBFGS")
+    obj._check_optimizer("Adam")

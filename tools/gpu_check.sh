@@ -1,7 +1,9 @@
 #!/bin/bash
-# GPU-box validation: smoke + parity tests (+ optional extra steps).  Each GPU
-# step has its own time limit; a crash/fault/timeout stops the script.
+# GPU-box validation: smoke + parity tests, then optional named steps given as
+# "name=command".  Each step has its own time limit; a crash, fault or timeout
+# (any rc other than 0/1) stops the script.
 mkdir -p gpurun_out
+: > gpurun_out/steps.log
 step() {  # step <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
   timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
@@ -9,8 +11,11 @@ step() {  # step <name> <seconds> <cmd...>
   echo "$name rc=$rc" | tee -a gpurun_out/steps.log
   case $rc in 0|1) return 0;; *) echo "stopping after $name (rc=$rc)"; exit $rc;; esac
 }
-step smoke 300 python __graft_entry__.py smoke
-step gpu_tests 600 python -m pytest tests -m gpu -x -q
+if [ -z "$SKIP_TESTS" ]; then
+  step smoke 300 python __graft_entry__.py smoke
+  step gpu_tests 600 python -m pytest tests -m gpu -x -q
+fi
+export TMPDIR=/tmp
 for extra in "$@"; do
-  step "$extra" 600 bash -c "$extra"
+  step "${extra%%=*}" 600 bash -c "${extra#*=}"
 done
