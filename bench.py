@@ -102,6 +102,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--activation", default="Sine", help="experiments only; the headline is Sine")
+    ap.add_argument("--mode", default="NAIS-Net", help="experiments only; the headline is NAIS-Net")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -117,7 +119,7 @@ def main():
     pkg = importlib.import_module(PKG)
     torch.manual_seed(0)
     Xi = np.array([1.0, 0.5] * (D // 2))[None, :]
-    model = pkg.BlackScholesBarenblatt(Xi, T, M_PER_GPU * world, N_STEPS, D, LAYERS, "NAIS-Net", "Sine",
+    model = pkg.BlackScholesBarenblatt(Xi, T, M_PER_GPU * world, N_STEPS, D, LAYERS, args.mode, args.activation,
                                        device=dev)
     opt = model.new_optimizer_state()
 
@@ -168,7 +170,7 @@ def main():
     dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
     name, st = dom
     avg_ms = st["ms"] / st["launches"]
-    is_mfma = name.startswith("gemm") or name.startswith("tn_")
+    is_mfma = name.startswith(("gemm", "tn_", "fused_"))
     if is_mfma:
         achieved = st["flops"] / st["launches"] / (avg_ms * 1e-3) / 1e12
         peak, unit = PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
@@ -199,7 +201,7 @@ def main():
         "data": "synthetic: device Philox Brownian increments, reference (xavier) init weights, seed 0",
         "config": {"workload": "100-D Black-Scholes-Barenblatt deep-BSDE training step "
                                "(DeepBSDE.py semantics: Adam lr 1e-3, no clip)",
-                   "D": D, "layers": LAYERS, "mode": "NAIS-Net", "activation": "Sine",
+                   "D": D, "layers": LAYERS, "mode": args.mode, "activation": args.activation,
                    "paths_per_gpu": M_PER_GPU, "global_batch": M_PER_GPU * world, "time_steps": N_STEPS,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma" if is_mfma else "hbm", "achieved": achieved, "peak": peak, "unit": unit,

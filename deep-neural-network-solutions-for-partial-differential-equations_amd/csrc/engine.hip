@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -22,6 +23,7 @@
 
 #include "../../include/dbsde.h"
 #include "kernels.hpp"
+#include "fused.hpp"
 
 using namespace dbsde;
 
@@ -29,7 +31,7 @@ namespace {
 
 thread_local std::string g_last_error;
 
-constexpr int TN_SPLITS = 32;   // fixed split count -> static slab layout
+constexpr int TN_SPLITS_MAX = 256;  // slab capacity; the split count is chosen per context
 
 inline int pad16(int x) { return (x + 15) / 16 * 16; }
 inline int padw(int x) { return x <= 128 ? pad16(x) : (x + 127) / 128 * 128; }
@@ -88,7 +90,7 @@ struct dbsde_ctx {
   PackDesc* d_fin = nullptr;
   int n_fin = 0;
   std::vector<float*> slab;  // TN problem slabs (0 = x-stack, j = block j)
-  std::vector<int> slab_mt, slab_nt;
+  std::vector<int> slab_mt, slab_nt, slab_mv, slab_nv;
   double* opt_part = nullptr;
   int opt_nparts = 0;
 
@@ -105,6 +107,10 @@ struct dbsde_ctx {
 
   std::vector<void*> allocs;      // fixed-size buffers
   std::vector<void*> row_allocs;  // buffers sized by the row count (regrown)
+
+  float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
+  bool fused = false;             // wave-level fused phase kernels usable for this net
+  int tn_splits = 32;              // weight-gradient GEMM row splits
 
   // ---- profiling
   bool prof = false;
@@ -187,6 +193,33 @@ int run(dbsde_ctx* c, const char* name, double flops, double bytes, F&& launch) 
     int rc_ = run(ctx, name, fl, by, [&]() { __VA_ARGS__; }); \
     if (rc_) return rc_;                                   \
   } while (0)
+
+// ---------------------------------------------------------------------------
+// fused phase-kernel instantiations: (level tiles T, D tiles TD, blocks K)
+struct FusedVariant {
+  int T, TD, K, act;
+  void (*A)(FusedArgs);
+  void (*C)(FusedArgs);
+};
+const FusedVariant kFused[] = {
+    {7, 7, 3, 0, phaseA_kernel<7, 7, 3, 0>, phaseC_kernel<7, 7, 3, 0>},
+    {7, 7, 3, 1, phaseA_kernel<7, 7, 3, 1>, phaseC_kernel<7, 7, 3, 1>},
+    {7, 7, 3, 2, phaseA_kernel<7, 7, 3, 2>, phaseC_kernel<7, 7, 3, 2>},
+    {1, 1, 1, 0, phaseA_kernel<1, 1, 1, 0>, phaseC_kernel<1, 1, 1, 0>},
+    {1, 1, 1, 1, phaseA_kernel<1, 1, 1, 1>, phaseC_kernel<1, 1, 1, 1>},
+    {1, 1, 1, 2, phaseA_kernel<1, 1, 1, 2>, phaseC_kernel<1, 1, 1, 2>},
+    {1, 1, 2, 0, phaseA_kernel<1, 1, 2, 0>, phaseC_kernel<1, 1, 2, 0>},
+    {1, 1, 2, 1, phaseA_kernel<1, 1, 2, 1>, phaseC_kernel<1, 1, 2, 1>},
+    {1, 1, 2, 2, phaseA_kernel<1, 1, 2, 2>, phaseC_kernel<1, 1, 2, 2>},
+    {1, 1, 3, 0, phaseA_kernel<1, 1, 3, 0>, phaseC_kernel<1, 1, 3, 0>},
+    {1, 1, 3, 1, phaseA_kernel<1, 1, 3, 1>, phaseC_kernel<1, 1, 3, 1>},
+    {1, 1, 3, 2, phaseA_kernel<1, 1, 3, 2>, phaseC_kernel<1, 1, 3, 2>},
+};
+int fused_variant(int T, int TD, int K, int act) {
+  for (int i = 0; i < (int)(sizeof(kFused) / sizeof(kFused[0])); ++i)
+    if (kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act) return i;
+  return -1;
+}
 
 // ---------------------------------------------------------------------------
 // network layout (state_dict order; oracle/timeparallel.param_layout mirrors it)
@@ -278,6 +311,11 @@ int build_net(dbsde_ctx* c) {
     c->Wmax = std::max(c->Wmax, c->Wp[j]);
   }
   c->Stot_x = c->has_v ? c->Stot : c->Wp[0];
+  bool uniform = true;
+  for (int j = 1; j <= c->K; ++j) uniform = uniform && c->Wp[j] == c->Wp[0];
+  const char* env = getenv("DBSDE_FUSED");
+  const bool allow = !(env && env[0] == '0');
+  c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act) >= 0;
   return DBSDE_OK;
 }
 
@@ -307,6 +345,7 @@ inline float* gtag(long long off) { return (float*)(kGradTag | (uintptr_t)(off *
 int build_buffers(dbsde_ctx* c) {
   const int K = c->K, D = c->D, Dp = c->Dp;
   int rc;
+  if (const char* e = getenv("DBSDE_TN_SPLITS")) c->tn_splits = std::max(1, std::min(TN_SPLITS_MAX, atoi(e)));
   if ((rc = dalloc_t(c, &c->BtIn, (size_t)c->Stot_x * Dp))) return rc;
   if ((rc = dalloc_t(c, &c->BtZ, (size_t)Dp * c->Stot_x))) return rc;
   if ((rc = dalloc_t(c, &c->wout, (size_t)c->Wp[K]))) return rc;
@@ -390,14 +429,20 @@ int build_buffers(dbsde_ctx* c) {
   c->slab.assign(K + 1, nullptr);
   c->slab_mt.assign(K + 1, 0);
   c->slab_nt.assign(K + 1, 0);
+  c->slab_mv.assign(K + 2, 0);
+  c->slab_nv.assign(K + 2, 0);
   auto mkslab = [&](int j, int m, int n) -> int {
+    c->slab_mv[j] = m;
+    c->slab_nv[j] = n;
     c->slab_mt[j] = (m + 63) / 64;
     c->slab_nt[j] = (n + 63) / 64;
-    return dalloc_t(c, &c->slab[j], (size_t)TN_SPLITS * c->slab_mt[j] * 64 * c->slab_nt[j] * 64);
+    return dalloc_t(c, &c->slab[j], (size_t)c->tn_splits * c->slab_mt[j] * 64 * c->slab_nt[j] * 64);
   };
   c->slab.resize(K + 2, nullptr);
   c->slab_mt.resize(K + 2, 0);
   c->slab_nt.resize(K + 2, 0);
+  c->slab_mv.resize(K + 2, 0);
+  c->slab_nv.resize(K + 2, 0);
   if ((rc = mkslab(0, c->Stot_x, Dp))) return rc;
   for (int j = 1; j <= K; ++j)
     if ((rc = mkslab(j, c->Wp[j], c->Wp[j - 1] + (c->has_v ? 0 : 1)))) return rc;
@@ -407,7 +452,7 @@ int build_buffers(dbsde_ctx* c) {
   auto slabsum = [&](int j, int r0, int c0, int rows, int cols, float* dst, int dst_ld, float scale) {
     const int ld = c->slab_nt[j] * 64;
     PackDesc d = mk_desc(c->slab[j] + (size_t)r0 * ld + c0, ld, dst, dst_ld, rows, cols, 0, PK_SLABSUM, scale);
-    d.nslab = TN_SPLITS;
+    d.nslab = c->tn_splits;
     d.slab_stride = (long long)c->slab_mt[j] * 64 * ld;
     F.push_back(d);
   };
@@ -477,7 +522,8 @@ int ensure_rows(dbsde_ctx* c, int Rp, int N) {
   if ((rc = dalloc_t(c, &c->o16, R * 16))) return rc;
   fill_col0_kernel<<<(unsigned)((R + 255) / 256), 256, 0, c->stream>>>(c->o16, 16, (long long)R, 1.f);
   HIPC(c, hipGetLastError());
-  if ((rc = dalloc_t(c, &c->loss_part, R / 256 + 2))) return rc;
+  if ((rc = dalloc_t(c, &c->loss_part, R / 16 + 2))) return rc;
+  if ((rc = dalloc_t(c, &c->rowsum, R * 8))) return rc;
   if ((rc = dalloc_t(c, &c->loss_tmp, 16))) return rc;
   if ((rc = dalloc_t(c, &c->q3S, (size_t)nn + 1))) return rc;
   c->row_allocs.assign(c->allocs.begin() + first, c->allocs.end());
@@ -666,7 +712,7 @@ int prep_weights(dbsde_ctx* c, const float* params) {
 
 int finalize_grads(dbsde_ctx* c, const float* params, float* grad) {
   hipStream_t s = c->stream;
-  RUN(c, "grad_finalize", 0.0, 0.0, pack_tagged_kernel<<<dim3(16, c->n_fin), 256, 0, s>>>(c->d_fin, params, grad));
+  RUN(c, "grad_finalize", 0.0, 0.0, pack_tagged_kernel<<<dim3(64, c->n_fin), 256, 0, s>>>(c->d_fin, params, grad));
   if (c->proj) {
     const int LW = c->L[1];
     const int nblk = (LW * LW + 255) / 256;
@@ -783,6 +829,50 @@ int validate_batch(dbsde_ctx* c, const dbsde_batch* b) {
   return DBSDE_OK;
 }
 
+int nv_x(dbsde_ctx* c) {
+  int nv = 0;
+  for (int j = 0; j <= (c->has_v ? c->K : 0); ++j) nv += c->L[j + 1];
+  return nv;
+}
+
+FusedArgs fused_args(dbsde_ctx* c, int R, int N1) {
+  FusedArgs a;
+  memset(&a, 0, sizeof(a));
+  a.R = R;
+  a.N1 = N1;
+  a.D = c->D;
+  a.Dp = c->Dp;
+  a.W = c->Wp[0];
+  a.S = c->Stot;
+  a.has_v = c->has_v;
+  a.act = c->act;
+  a.rho = c->rho;
+  a.xin = c->xin;
+  a.BtIn = c->BtIn;
+  a.BtZ = c->BtZ;
+  a.ldz = c->Stot_x;
+  for (int j = 1; j <= c->K; ++j) {
+    a.Bf[j - 1] = c->Bf[j];
+    a.Bb[j - 1] = c->Bb[j];
+    a.beta[j - 1] = c->beta[j];
+  }
+  a.wout = c->wout;
+  a.bout = c->bout;
+  a.Abuf = c->Abuf;
+  a.H = c->H;
+  a.G = c->G;
+  a.Delta = c->Delta;
+  a.u = c->u;
+  a.zfull = c->zfull;
+  a.rowsum = c->rowsum;
+  a.sdw = c->sdw;
+  a.zbar = c->zbar;
+  a.ubar = c->ubar;
+  a.Hdot = c->Hdot;
+  a.Alpha = c->Alpha;
+  return a;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -892,117 +982,160 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   const bool q3 = pr.q3 && D == 1;
   if (q3) RUN(c, "q3_sum", 0.0, 4.0 * M * N, q3_sum_kernel<<<N, 256, 0, s>>>(c->sdw, c->Dp, M, N, c->q3S));
 
-  if ((rc = forward_and_inputgrad(c, R, Rp, false))) return rc;
+  int nloss_parts;
+  FusedArgs fa;
+  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act) : -1;
+  if (fv >= 0) {
+    fa = fused_args(c, R, N1);
+    const int nv = nv_x(c);
+    const double flA = 2.0 * R * ((D + 1.0) * nv + 2.0 * K * L[1] * (double)L[1] + (double)nv * D);
+    RUN(c, "fused_fwd_inputgrad", flA, 4.0 * R * (c->Dp + 4.0 * S + 8.0),
+        kFused[fv].A<<<Rp / 64, 256, 0, s>>>(fa));
+    CotanArgs ca{};
+    ca.R = R;
+    ca.Rp = Rp;
+    ca.N1 = N1;
+    ca.D = D;
+    ca.Dp = c->Dp;
+    ca.xin = c->xin;
+    ca.sdw = c->sdw;
+    ca.zfull = c->zfull;
+    ca.u = c->u;
+    ca.rowsum = c->rowsum;
+    ca.q3S = q3 ? c->q3S : nullptr;
+    ca.phi_r = pr.phi_r;
+    ca.phi_c = pr.phi_c;
+    ca.phi_zz = pr.phi_zz;
+    ca.strike = pr.strike;
+    ca.g_kind = pr.g_kind;
+    ca.zbar = c->zbar;
+    ca.ubar = c->ubar;
+    ca.u16 = c->u16;
+    ca.lossrow = c->lossrow;
+    ca.loss_part = c->loss_part;
+    RUN(c, "cotangent", 0.0, 4.0 * R * 5.0 * D, cotan_kernel<<<Rp / 16, 256, 0, s>>>(ca));
+    nloss_parts = Rp / 16;
+  } else {
+    if ((rc = forward_and_inputgrad(c, R, Rp, false))) return rc;
 
-  // ---- Z GEMM + residuals / cotangents / loss rows
-  {
-    ChainArgs a = base_args(c);
-    zgemm_args(c, a);
-    a.R = R;
-    a.N1 = N1;
-    a.D = D;
-    a.xin = c->xin;
-    a.sdw = c->sdw;
-    a.ldx = c->Dp;
-    a.u = c->u;
-    a.q3S = q3 ? c->q3S : nullptr;
-    a.phi_r = pr.phi_r;
-    a.phi_c = pr.phi_c;
-    a.phi_zz = pr.phi_zz;
-    a.strike = pr.strike;
-    a.g_kind = pr.g_kind;
-    a.zbar = c->zbar;
-    a.rres = c->rres;
-    a.lossrow = c->lossrow;
-    if ((rc = chain<EPI_COTAN>(c, "gemm_z_cotangent", a, Rp, c->Dp, c->Dp / 16, zgemm_flops(c, R),
-                               4.0 * R * (c->Stot_x + 5.0 * D))))
-      return rc;
-  }
-  RUN(c, "ubar_loss", 0.0, 16.0 * R,
-      ubar_kernel<<<Rp / 256 + 1, 256, 0, s>>>(c->rres, c->xin, c->Dp, R, Rp, N1, pr.phi_r, c->lossrow, c->ubar,
-                                               c->u16, c->loss_part));
-  float* loss_dst = (out && out->loss) ? out->loss : c->loss_tmp;
-  RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, s>>>(c->loss_part, Rp / 256 + 1, loss_dst));
-
-  if (grad) {
-    // ---- forward tangent along zbar
+    // ---- Z GEMM + residuals / cotangents / loss rows
     {
       ChainArgs a = base_args(c);
-      a.A = c->zbar;
-      a.lda = c->Dp;
-      a.Bt = c->BtIn;
-      a.ldb = c->Dp;
-      a.K = c->Dp;
-      a.in[0] = c->Abuf;
-      a.ldi[0] = S;
-      a.out[0] = c->Adot;
-      a.ldo[0] = S;
-      a.out[1] = c->Hdot;
-      a.ldo[1] = S;
-      a.lvl0_cols = c->Wp[0];
-      int nv = 0;
-      for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
-      if ((rc = chain<EPI_TAN0>(c, "gemm_xstack_tangent", a, Rp, c->Stot_x, nt_for(c->Wp[0]),
-                                2.0 * R * D * nv, 4.0 * R * (D + 2.0 * nv + L[1]))))
+      zgemm_args(c, a);
+      a.R = R;
+      a.N1 = N1;
+      a.D = D;
+      a.xin = c->xin;
+      a.sdw = c->sdw;
+      a.ldx = c->Dp;
+      a.u = c->u;
+      a.q3S = q3 ? c->q3S : nullptr;
+      a.phi_r = pr.phi_r;
+      a.phi_c = pr.phi_c;
+      a.phi_zz = pr.phi_zz;
+      a.strike = pr.strike;
+      a.g_kind = pr.g_kind;
+      a.zbar = c->zbar;
+      a.rres = c->rres;
+      a.lossrow = c->lossrow;
+      if ((rc = chain<EPI_COTAN>(c, "gemm_z_cotangent", a, Rp, c->Dp, c->Dp / 16, zgemm_flops(c, R),
+                                 4.0 * R * (c->Stot_x + 5.0 * D))))
         return rc;
     }
-    for (int j = 1; j <= K; ++j) {
-      ChainArgs a = base_args(c);
-      a.A = c->Hdot + c->col[j - 1];
-      a.lda = S;
-      a.Bt = c->Bf[j];
-      a.ldb = c->Wp[j - 1];
-      a.K = c->Wp[j - 1];
-      a.in[0] = c->has_v ? c->Adot + c->col[j] : nullptr;
-      a.ldi[0] = S;
-      a.in[1] = c->Hdot + c->col[j - 1];
-      a.ldi[1] = S;
-      a.in[2] = c->Abuf + c->col[j];
-      a.ldi[2] = S;
-      a.out[0] = c->Adot + c->col[j];
-      a.ldo[0] = S;
-      a.out[1] = c->Hdot + c->col[j];
-      a.ldo[1] = S;
-      a.last = j == K;
-      a.out[2] = c->Alpha + c->col[K];
-      a.ldo[2] = S;
-      a.vec[0] = c->wout;
-      a.ubar = c->ubar;
-      if ((rc = chain<EPI_TAN>(c, "gemm_block_tangent", a, Rp, c->Wp[j], nt_for(c->Wp[j]),
-                               2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j] + 6.0 * L[j + 1]))))
-        return rc;
-    }
-    // ---- reverse over (primal, tangent)
-    for (int j = K; j >= 1; --j) {
-      ChainArgs a = base_args(c);
-      a.A = c->Alpha + c->col[j];
-      a.lda = S;
-      a.Bt = c->Bb[j];
-      a.ldb = c->Wp[j];
-      a.K = c->Wp[j];
-      a.in[0] = j == K ? nullptr : c->Pbuf[(j + 1) & 1];
-      a.ldi[0] = c->Wmax;
-      a.ubar = c->ubar;
-      a.vec[0] = c->wout;
-      a.in[1] = c->Abuf + c->col[j - 1];
-      a.ldi[1] = S;
-      a.in[2] = c->G + c->col[j - 1];
-      a.ldi[2] = S;
-      a.in[3] = c->Adot + c->col[j - 1];
-      a.ldi[3] = S;
-      a.out[0] = c->Pbuf[j & 1];
-      a.ldo[0] = c->Wmax;
-      a.out[1] = c->Alpha + c->col[j - 1];
-      a.ldo[1] = S;
-      if ((rc = chain<EPI_REV>(c, "gemm_block_reverse", a, Rp, c->Wp[j - 1], nt_for(c->Wp[j - 1]),
-                               2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j + 1] + 6.0 * L[j]))))
-        return rc;
+    RUN(c, "ubar_loss", 0.0, 16.0 * R,
+        ubar_kernel<<<Rp / 256 + 1, 256, 0, s>>>(c->rres, c->xin, c->Dp, R, Rp, N1, pr.phi_r, c->lossrow, c->ubar,
+                                                 c->u16, c->loss_part));
+    nloss_parts = Rp / 256 + 1;
+  }
+  float* loss_dst = (out && out->loss) ? out->loss : c->loss_tmp;
+  RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, s>>>(c->loss_part, nloss_parts, loss_dst));
+
+  if (grad) {
+    if (fv >= 0) {
+      const int nv = nv_x(c);
+      const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
+      RUN(c, "fused_tangent_reverse", flC, 4.0 * R * (c->Dp + 5.0 * S), kFused[fv].C<<<Rp / 64, 256, 0, s>>>(fa));
+    } else {
+      // ---- forward tangent along zbar
+      {
+        ChainArgs a = base_args(c);
+        a.A = c->zbar;
+        a.lda = c->Dp;
+        a.Bt = c->BtIn;
+        a.ldb = c->Dp;
+        a.K = c->Dp;
+        a.in[0] = c->Abuf;
+        a.ldi[0] = S;
+        a.out[0] = c->Adot;
+        a.ldo[0] = S;
+        a.out[1] = c->Hdot;
+        a.ldo[1] = S;
+        a.lvl0_cols = c->Wp[0];
+        int nv = 0;
+        for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
+        if ((rc = chain<EPI_TAN0>(c, "gemm_xstack_tangent", a, Rp, c->Stot_x, nt_for(c->Wp[0]),
+                                  2.0 * R * D * nv, 4.0 * R * (D + 2.0 * nv + L[1]))))
+          return rc;
+      }
+      for (int j = 1; j <= K; ++j) {
+        ChainArgs a = base_args(c);
+        a.A = c->Hdot + c->col[j - 1];
+        a.lda = S;
+        a.Bt = c->Bf[j];
+        a.ldb = c->Wp[j - 1];
+        a.K = c->Wp[j - 1];
+        a.in[0] = c->has_v ? c->Adot + c->col[j] : nullptr;
+        a.ldi[0] = S;
+        a.in[1] = c->Hdot + c->col[j - 1];
+        a.ldi[1] = S;
+        a.in[2] = c->Abuf + c->col[j];
+        a.ldi[2] = S;
+        a.out[0] = c->Adot + c->col[j];
+        a.ldo[0] = S;
+        a.out[1] = c->Hdot + c->col[j];
+        a.ldo[1] = S;
+        a.last = j == K;
+        a.out[2] = c->Alpha + c->col[K];
+        a.ldo[2] = S;
+        a.vec[0] = c->wout;
+        a.ubar = c->ubar;
+        if ((rc = chain<EPI_TAN>(c, "gemm_block_tangent", a, Rp, c->Wp[j], nt_for(c->Wp[j]),
+                                 2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j] + 6.0 * L[j + 1]))))
+          return rc;
+      }
+      // ---- reverse over (primal, tangent)
+      for (int j = K; j >= 1; --j) {
+        ChainArgs a = base_args(c);
+        a.A = c->Alpha + c->col[j];
+        a.lda = S;
+        a.Bt = c->Bb[j];
+        a.ldb = c->Wp[j];
+        a.K = c->Wp[j];
+        a.in[0] = j == K ? nullptr : c->Pbuf[(j + 1) & 1];
+        a.ldi[0] = c->Wmax;
+        a.ubar = c->ubar;
+        a.vec[0] = c->wout;
+        a.in[1] = c->Abuf + c->col[j - 1];
+        a.ldi[1] = S;
+        a.in[2] = c->G + c->col[j - 1];
+        a.ldi[2] = S;
+        a.in[3] = c->Adot + c->col[j - 1];
+        a.ldi[3] = S;
+        a.out[0] = c->Pbuf[j & 1];
+        a.ldo[0] = c->Wmax;
+        a.out[1] = c->Alpha + c->col[j - 1];
+        a.ldo[1] = S;
+        if ((rc = chain<EPI_REV>(c, "gemm_block_reverse", a, Rp, c->Wp[j - 1], nt_for(c->Wp[j - 1]),
+                                 2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j + 1] + 6.0 * L[j]))))
+          return rc;
+      }
     }
     // ---- parameter gradients
     HIPC(c, hipMemsetAsync(grad, 0, (size_t)c->nparams * 4, s));
     TNArgs ta;
     memset(&ta, 0, sizeof(ta));
-    const int rps = ((Rp + TN_SPLITS - 1) / TN_SPLITS + TN_KC - 1) / TN_KC * TN_KC;
+    const int S_ = c->tn_splits;
+    const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
     ta.rows_per_split = rps;
     ta.Rp = Rp;
     double tfl = 0.0;
@@ -1022,6 +1155,8 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
       p0.nB[1] = c->Dp;
       p0.npairs = 2;
       p0.ones_col = -1;
+      p0.mv = c->slab_mv[0];
+      p0.nv = c->slab_nv[0];
       p0.mt = c->slab_mt[0];
       p0.nt = c->slab_nt[0];
       p0.slab = c->slab[0];
@@ -1046,6 +1181,8 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
       pj.nB[1] = c->Wp[j - 1];
       pj.npairs = 2;
       pj.ones_col = c->has_v ? -1 : c->Wp[j - 1];
+      pj.mv = c->slab_mv[j];
+      pj.nv = c->slab_nv[j];
       pj.mt = c->slab_mt[j];
       pj.nt = c->slab_nt[j];
       pj.slab = c->slab[j];
@@ -1069,6 +1206,8 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
       po.nB[1] = c->Wp[K];
       po.npairs = 2;
       po.ones_col = c->Wp[K];
+      po.mv = 1;
+      po.nv = c->slab_nv[K + 1];
       po.mt = c->slab_mt[K + 1];
       po.nt = c->slab_nt[K + 1];
       po.slab = c->slab[K + 1];
@@ -1076,7 +1215,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
       tfl += 2.0 * 2.0 * R * (L[K + 1] + 1);
     }
     if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
-    RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, TN_SPLITS, K + 2), 256, 0, s>>>(ta));
+    RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
     if ((rc = finalize_grads(c, params, grad))) return rc;
   }
 

@@ -20,13 +20,39 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 enum Act { ACT_SINE = 0, ACT_RELU = 1, ACT_TANH = 2 };
 
+// sin and cos together: quadrant reduction in fp64 (exact enough for any
+// activation magnitude that can occur), cephes minimax polynomials in fp32 on
+// [-pi/4, pi/4].  Max abs error < 0.8 * 2^-23 for |a| <= 2e4 (host-tested
+// against libm in fp64, tests/test_host_logic.py mirrors it in numpy).  Far
+// fewer registers than the library sincosf, whose large-argument path is
+// allocated for every unrolled element.
+__device__ __forceinline__ void fast_sincosf(float a, float& s, float& c) {
+  const double k = rint((double)a * 0.63661977236758134308);
+  const float r = (float)fma(-k, 1.5707963267948966192, (double)a);
+  const int m = (int)(long long)k & 3;
+  const float z = r * r;
+  const float sp = r + r * z * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
+  const float cp =
+      1.0f - 0.5f * z + z * z * (4.166664568298827e-2f + z * (-1.388731625493765e-3f + z * 2.443315711809948e-5f));
+  s = (m == 0) ? sp : (m == 1) ? cp : (m == 2) ? -sp : -cp;
+  c = (m == 0) ? cp : (m == 1) ? -sp : (m == 2) ? -cp : sp;
+}
+
 __device__ __forceinline__ float act_f(int act, float a) {
-  if (act == ACT_SINE) return sinf(a);
+  if (act == ACT_SINE) {
+    float sv, cv;
+    fast_sincosf(a, sv, cv);
+    return sv;
+  }
   if (act == ACT_TANH) return tanhf(a);
   return a > 0.f ? a : 0.f;
 }
 __device__ __forceinline__ float act_d1(int act, float a) {
-  if (act == ACT_SINE) return cosf(a);
+  if (act == ACT_SINE) {
+    float sv, cv;
+    fast_sincosf(a, sv, cv);
+    return cv;
+  }
   if (act == ACT_TANH) {
     float t = tanhf(a);
     return 1.f - t * t;
@@ -36,7 +62,7 @@ __device__ __forceinline__ float act_d1(int act, float a) {
 __device__ __forceinline__ void act_d12(int act, float a, float& d1, float& d2) {
   if (act == ACT_SINE) {
     float s, c;
-    sincosf(a, &s, &c);
+    fast_sincosf(a, s, c);
     d1 = c;
     d2 = -s;
   } else if (act == ACT_TANH) {
@@ -510,6 +536,7 @@ struct TNProb {
   int ldb[2], nB[2];
   int npairs;
   int ones_col;   // pair-0 B column treated as 1.0 (bias gradient); -1 none
+  int mv, nv;     // valid output extent
   int mt, nt;     // tiles of 64
   float* slab;    // [splits][mt*64][nt*64]
 };
@@ -533,8 +560,11 @@ __global__ void __launch_bounds__(256) tn_gemm_kernel(TNArgs args) {
   if (r_end > args.Rp) r_end = args.Rp;
   __shared__ float As[2][TN_KC * TN_LS];
   __shared__ float Bs[2][TN_KC * TN_LS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
+  // a wave whose 32x32 quadrant lies outside the valid output skips its MFMAs
+  const bool active = (tm * 64 + wm * 32 < P.mv) && (tn * 64 + wn * 32 < P.nv);
   floatx4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -554,7 +584,10 @@ __global__ void __launch_bounds__(256) tn_gemm_kernel(TNArgs args) {
       br = *(const floatx4*)(P.B[pr] + r * P.ldb[pr] + cb);
     } else {
       br = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (pr == 0 && P.ones_col >= cb && P.ones_col < cb + 4) br[P.ones_col - cb] = 1.f;
+      if (pr == 0 && P.ones_col >= cb && P.ones_col < cb + 4) {
+        const int o = P.ones_col - cb;
+        br = floatx4{o == 0 ? 1.f : 0.f, o == 1 ? 1.f : 0.f, o == 2 ? 1.f : 0.f, o == 3 ? 1.f : 0.f};
+      }
     }
   };
   auto sstore = [&](int buf) {
@@ -568,19 +601,21 @@ __global__ void __launch_bounds__(256) tn_gemm_kernel(TNArgs args) {
     for (int it = 0; it < total; ++it) {
       const int buf = it & 1;
       if (it + 1 < total) gload(it + 1);
+      if (active) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = 4 * i + (lane >> 4);
-        float a[2], b[2];
+        for (int i = 0; i < 4; ++i) {
+          const int k = 4 * i + (lane >> 4);
+          float a[2], b[2];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          a[s] = As[buf][k * TN_LS + wm * 32 + s * 16 + (lane & 15)];
-          b[s] = Bs[buf][k * TN_LS + wn * 32 + s * 16 + (lane & 15)];
+          for (int s = 0; s < 2; ++s) {
+            a[s] = As[buf][k * TN_LS + wm * 32 + s * 16 + (lane & 15)];
+            b[s] = Bs[buf][k * TN_LS + wn * 32 + s * 16 + (lane & 15)];
+          }
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc[x][y] = mfma4(a[x], b[y], acc[x][y]);
         }
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-          for (int y = 0; y < 2; ++y) acc[x][y] = mfma4(a[x], b[y], acc[x][y]);
       }
       if (it + 1 < total) sstore(buf ^ 1);
       __syncthreads();

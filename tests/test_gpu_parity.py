@@ -51,11 +51,26 @@ def dev():
     return torch.device("cuda:0")
 
 
-def native_case(pkg, dev, g, want_grad=True):
+def make_solver(pkg, dev, g, fused=True):
+    """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at create)."""
+    layers = [int(v) for v in g["layers"]]
+    D = layers[0] - 1
+    old = os.environ.get("DBSDE_FUSED")
+    os.environ["DBSDE_FUSED"] = "1" if fused else "0"
+    try:
+        return pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]), spec_for(pkg, str(g["problem"]), D),
+                                float(g["T"]), dev)
+    finally:
+        if old is None:
+            del os.environ["DBSDE_FUSED"]
+        else:
+            os.environ["DBSDE_FUSED"] = old
+
+
+def native_case(pkg, dev, g, want_grad=True, fused=True):
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
-    s = pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]), spec_for(pkg, str(g["problem"]), D),
-                         float(g["T"]), dev)
+    s = make_solver(pkg, dev, g, fused)
     params = torch.from_numpy(g["params"]).to(dev)
     out = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (N + 1) * D, device=dev),
                Y=torch.empty(M * (N + 1), device=dev), Z=torch.empty(M * (N + 1) * D, device=dev))
@@ -73,10 +88,11 @@ def native_case(pkg, dev, g, want_grad=True):
     return res
 
 
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "chain"])
 @pytest.mark.parametrize("path", G1, ids=[os.path.basename(p)[3:-4] for p in G1])
-def test_loss_grad_matches_reference(pkg, dev, path):
+def test_loss_grad_matches_reference(pkg, dev, path, fused):
     g = _load(path)
-    r = native_case(pkg, dev, g)
+    r = native_case(pkg, dev, g, fused=fused)
     np.testing.assert_array_equal(r["X"], g["X"])
     np.testing.assert_allclose(r["loss"][0], g["loss"], rtol=1e-4)
     np.testing.assert_allclose(r["Y"], g["Y"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Y"]).max()))
@@ -93,10 +109,11 @@ def test_forward_only_matches(pkg, dev, path):
     np.testing.assert_allclose(r["loss"][0], g["loss"], rtol=1e-4)
 
 
-def test_repeatable(pkg, dev):
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "chain"])
+def test_repeatable(pkg, dev, fused):
     g = _load(G1[0])
-    a = native_case(pkg, dev, g)
-    b = native_case(pkg, dev, g)
+    a = native_case(pkg, dev, g, fused=fused)
+    b = native_case(pkg, dev, g, fused=fused)
     np.testing.assert_array_equal(a["grad"], b["grad"])     # deterministic reductions (no atomics)
     np.testing.assert_array_equal(a["loss"], b["loss"])
 
@@ -185,3 +202,27 @@ def test_net_u_matches_fixture_Y(pkg, dev):
     torch.cuda.synchronize()
     np.testing.assert_allclose(u.cpu().numpy(), g["Y"].reshape(R), rtol=0, atol=1e-4)
     np.testing.assert_allclose(du.cpu().numpy(), g["Z"].reshape(R, D), rtol=0, atol=1e-4)
+
+
+def test_fused_and_chain_paths_agree_at_north_star(pkg, dev):
+    """Both kernel paths on the full north-star batch (same params and W)."""
+    g = _load(os.path.join(GOLDEN, "g2_north_star.npz"))
+    layers = [int(v) for v in g["layers"]]
+    D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
+    rs = np.random.RandomState(7)
+    W = np.cumsum(np.concatenate([np.zeros((M, 1, D)), np.sqrt(1 / N) * rs.normal(size=(M, N, D))], 1), 1)
+    t = np.cumsum(np.concatenate([np.zeros((M, 1)), np.full((M, N), 1 / N)], 1), 1)
+    res = []
+    for fused in (True, False):
+        s = make_solver(pkg, dev, g, fused)
+        params = torch.from_numpy(g["params"]).to(dev)
+        grad, loss = torch.empty_like(params), torch.empty(1, device=dev)
+        Y = torch.empty(M * (N + 1), device=dev)
+        s.loss_grad(params, M, N, torch.from_numpy(g["Xi"]).to(dev), t=torch.from_numpy(t).float().to(dev),
+                    W=torch.from_numpy(W).float().to(dev), grad=grad, loss=loss, Y=Y)
+        torch.cuda.synchronize()
+        res.append((float(loss), grad.cpu().numpy(), Y.cpu().numpy()))
+    (l1, g1, y1), (l2, g2, y2) = res
+    assert abs(l1 - l2) <= 1e-5 * abs(l2)
+    np.testing.assert_allclose(y1, y2, rtol=0, atol=1e-4)
+    np.testing.assert_allclose(g1, g2, rtol=0, atol=1e-4 * np.abs(g2).max())
