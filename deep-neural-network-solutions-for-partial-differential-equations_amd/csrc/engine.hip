@@ -110,7 +110,7 @@ struct dbsde_ctx {
 
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
-  int tn_splits = 32;              // weight-gradient GEMM row splits
+  int tn_splits = 96;              // weight-gradient GEMM row splits (A/B: 64..128 best on MI355X)
 
   // ---- profiling
   bool prof = false;
@@ -373,7 +373,8 @@ int build_buffers(dbsde_ctx* c) {
       ha[j - 1] = c->abar[j];
       hw[j - 1] = c->B[j - 1].w;
     }
-    if ((rc = dalloc_t(c, &c->proj_part, (size_t)K * ((LW * LW + 255) / 256)))) return rc;
+    if ((rc = dalloc_t(c, &c->proj_part, (size_t)K * std::max((LW * LW + 255) / 256, ((LW + 15) / 16) * ((LW + 15) / 16)))))
+      return rc;
     if ((rc = dalloc_t(c, &c->d_rtr, K))) return rc;
     if ((rc = dalloc_t(c, &c->d_abar, K))) return rc;
     if ((rc = dalloc_t(c, &c->d_sbuf, K))) return rc;
@@ -603,9 +604,17 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
       a = a + (r == cc ? 0.01f : 0.f);
       v = -a;
     } else {
-      double s = 0.0;
-      for (int k = 0; k < d.nslab; ++k) s += d.src[k * d.slab_stride + (size_t)r * d.src_ld + cc];
-      v = d.scale * (float)s;
+      const float* src = d.src + (size_t)r * d.src_ld + cc;
+      double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      int k = 0;
+      for (; k + 8 <= d.nslab; k += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sa[u] += src[(size_t)(k + u) * d.slab_stride];
+      }
+      for (; k < d.nslab; ++k) sa[0] += src[(size_t)k * d.slab_stride];
+      const double s0 = (sa[0] + sa[1]) + (sa[2] + sa[3]), s1 = (sa[4] + sa[5]) + (sa[6] + sa[7]);
+      const double s2 = 0.0, s3 = 0.0;
+      v = d.scale * (float)((s0 + s1) + (s2 + s3));
     }
     if (d.transpose)
       d.dst[(size_t)cc * d.dst_ld + r] = v;
@@ -613,20 +622,45 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
       d.dst[(size_t)r * d.dst_ld + cc] = v;
   }
 }
-// RtR_j = W_j^T W_j (Functions/naisnet.py:33), one thread per element, and
-// per-block partial sums of squares for the Frobenius norm (fixed order).
+// Small LDS-tiled SGEMM for the L x L NAIS matrices (L <= 128): one 16x16
+// output tile per 256-thread workgroup, K staged through LDS in 16-wide tiles.
+//   TRANS_A: C = A^T B (RtR = W^T W)   else: C = A B (Wbar = W S)
+template <bool TRANS_A>
+__device__ __forceinline__ float tile_gemm16(const float* A, const float* B, int L, int ti, int tj, float (*As)[17],
+                                             float (*Bs)[17]) {
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int row = ti * 16 + ty, col = tj * 16 + tx;
+  float acc = 0.f;
+  for (int k0 = 0; k0 < L; k0 += 16) {
+    const int kr = k0 + tx, kc = k0 + ty;
+    // As[ty][tx] = op(A)[row][k0+tx], Bs[ty][tx] = B[k0+ty][col]
+    if (TRANS_A)
+      As[ty][tx] = (row < L && kr < L) ? A[kr * L + row] : 0.f;
+    else
+      As[ty][tx] = (row < L && kr < L) ? A[row * L + kr] : 0.f;
+    Bs[ty][tx] = (kc < L && col < L) ? B[kc * L + col] : 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += As[ty][k] * Bs[k][tx];
+    __syncthreads();
+  }
+  return acc;
+}
+
+// RtR_j = W_j^T W_j (Functions/naisnet.py:33) and per-tile partial sums of
+// squares for the Frobenius norm (fixed order).
 __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, const long long* woffs, int L,
                                                          float* const* rtr, double* part, int nblk) {
-  const int j = blockIdx.y;
+  __shared__ float As[16][17], Bs[16][17];
+  const int j = blockIdx.y, nt = (L + 15) / 16;
+  const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
   const float* W = params + woffs[j];
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const float v = tile_gemm16<true>(W, W, L, ti, tj, As, Bs);
+  const int row = ti * 16 + (threadIdx.x >> 4), col = tj * 16 + (threadIdx.x & 15);
   double sq = 0.0;
-  if (i < L * L) {
-    const int a = i / L, b = i - a * L;
-    float s = 0.f;
-    for (int k = 0; k < L; ++k) s += W[k * L + a] * W[k * L + b];
-    rtr[j][i] = s;
-    sq = (double)s * (double)s;
+  if (row < L && col < L) {
+    rtr[j][row * L + col] = v;
+    sq = (double)v * (double)v;
   }
   __shared__ double red[256];
   red[threadIdx.x] = sq;
@@ -679,18 +713,15 @@ __global__ void __launch_bounds__(256) proj_s_kernel(float* const* abar, float* 
   const float* R = rtr[j];
   sbuf[j][i] = cA * (Ab[a * L + b] + Ab[b * L + a]) - cR * (R[a * L + b] + R[b * L + a]);
 }
-// Wbar_j = W_j S_j  -> grad (one thread per element)
+// Wbar_j = W_j S_j  -> grad
 __global__ void __launch_bounds__(256) proj_wbar_kernel(const float* params, const long long* woffs,
                                                         float* const* sbuf, int L, float* grad) {
-  const int j = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= L * L) return;
-  const int a = i / L, b = i - a * L;
-  const float* W = params + woffs[j];
-  const float* S = sbuf[j];
-  float s = 0.f;
-  for (int k = 0; k < L; ++k) s += W[a * L + k] * S[k * L + b];
-  grad[woffs[j] + i] = s;
+  __shared__ float As[16][17], Bs[16][17];
+  const int j = blockIdx.y, nt = (L + 15) / 16;
+  const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
+  const float v = tile_gemm16<false>(params + woffs[j], sbuf[j], L, ti, tj, As, Bs);
+  const int row = ti * 16 + (threadIdx.x >> 4), col = tj * 16 + (threadIdx.x & 15);
+  if (row < L && col < L) grad[woffs[j] + row * L + col] = v;
 }
 }  // namespace dbsde
 
@@ -701,7 +732,7 @@ int prep_weights(dbsde_ctx* c, const float* params) {
   const int LW = c->L[1];
   if (c->proj) {
     const double fl = 2.0 * c->K * LW * (double)LW * LW;
-    const int nblk = (LW * LW + 255) / 256;
+    const int nblk = ((LW + 15) / 16) * ((LW + 15) / 16);
     RUN(c, "rtr", fl, 0.0,
         rtr_params_kernel<<<dim3(nblk, c->K), 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, c->proj_part, nblk));
     RUN(c, "rtr_norm", 0.0, 0.0, norm_from_parts_kernel<<<1, 64, 0, s>>>(c->proj_part, nblk, c->K, c->norms));
@@ -720,8 +751,9 @@ int finalize_grads(dbsde_ctx* c, const float* params, float* grad) {
     RUN(c, "proj_dot", 0.0, 0.0, proj_dot_kernel<<<g, 256, 0, s>>>(c->d_abar, c->d_rtr, LW, c->proj_part, nblk));
     RUN(c, "proj_s", 0.0, 0.0,
         proj_s_kernel<<<g, 256, 0, s>>>(c->d_abar, c->d_rtr, c->d_sbuf, LW, c->proj_part, nblk, c->norms));
+    const int ntile = ((LW + 15) / 16) * ((LW + 15) / 16);
     RUN(c, "proj_wbar", 2.0 * c->K * LW * (double)LW * LW, 0.0,
-        proj_wbar_kernel<<<g, 256, 0, s>>>(params, c->d_woffs, c->d_sbuf, LW, grad));
+        proj_wbar_kernel<<<dim3(ntile, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_sbuf, LW, grad));
   }
   return DBSDE_OK;
 }

@@ -161,7 +161,7 @@ __device__ __forceinline__ void wave_gemm(Mat<TO>& acc, const float* Al, int lda
 // Workgroup-cooperative variant: the 4 waves of a workgroup (64 rows) share
 // each 16-deep chunk of Bt through a double-buffered LDS stage (Bs holds
 // 2 x [16*TO][FB_LS] floats); A stays per wave.  Every wave must call it.
-constexpr int FB_LS = 20;
+constexpr int FB_LS = 24;   // = 8 mod 16: conflict-free ds_read_b128 fragment reads (gfx950 lane groups)
 template <int TO>
 __device__ __forceinline__ void wg_gemm(Mat<TO>& acc, const float* Al, int lda, int K, const float* Bt, int ldb,
                                         int kofs, float* Bs) {
@@ -190,8 +190,12 @@ __device__ __forceinline__ void wg_gemm(Mat<TO>& acc, const float* Al, int lda, 
   __syncthreads();
   const float* ap = Al + cl * lda + 4 * q;
   for (int c = 0; c < nc; ++c) {
+#ifdef DBSDE_EXP_NOBSTAGE
+    const int b = 0;   // timing experiment only: reuse chunk 0, no staging, no barrier
+#else
     const int b = c & 1;
     if (c + 1 < nc) gl(c + 1);
+#endif
     const floatx4 a = *(const floatx4*)(ap + 16 * c);
     floatx4 bv[TO];
 #pragma unroll
@@ -204,8 +208,10 @@ __device__ __forceinline__ void wg_gemm(Mat<TO>& acc, const float* Al, int lda, 
     for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.z, bv[t].z, acc.v[t]);
 #pragma unroll
     for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.w, bv[t].w, acc.v[t]);
+#ifndef DBSDE_EXP_NOBSTAGE
     if (c + 1 < nc) ls(b ^ 1);
     __syncthreads();
+#endif
   }
 }
 
@@ -218,6 +224,9 @@ __device__ __forceinline__ void zero(Mat<TT>& m) {
 // accumulator-layout tile <-> global row-major matrix
 template <int TT>
 __device__ __forceinline__ void gstore(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
+#ifdef DBSDE_EXP_NOSTORE
+  if (base != nullptr) return;   // timing experiment only: activation stores dropped
+#endif
   const int lane = threadIdx.x & 63, cl = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int t = 0; t < TT; ++t)

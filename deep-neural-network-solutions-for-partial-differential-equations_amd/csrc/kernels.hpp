@@ -20,16 +20,25 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 enum Act { ACT_SINE = 0, ACT_RELU = 1, ACT_TANH = 2 };
 
-// sin and cos together: quadrant reduction in fp64 (exact enough for any
-// activation magnitude that can occur), cephes minimax polynomials in fp32 on
+// sin and cos together: Cody-Waite reduction with a 3-part pi/2 in fp32 for
+// |a| <= 8192 (fp64 reduction above), cephes minimax polynomials in fp32 on
 // [-pi/4, pi/4].  Max abs error < 0.8 * 2^-23 for |a| <= 2e4 (host-tested
-// against libm in fp64, tests/test_host_logic.py mirrors it in numpy).  Far
-// fewer registers than the library sincosf, whose large-argument path is
-// allocated for every unrolled element.
+// against libm in fp64).  Far fewer registers and VALU cycles than the library
+// sincosf, whose large-argument path is allocated for every unrolled element.
 __device__ __forceinline__ void fast_sincosf(float a, float& s, float& c) {
-  const double k = rint((double)a * 0.63661977236758134308);
-  const float r = (float)fma(-k, 1.5707963267948966192, (double)a);
-  const int m = (int)(long long)k & 3;
+  float r;
+  int m;
+  if (__builtin_expect(fabsf(a) <= 8192.f, 1)) {
+    const float k = rintf(a * 0.636619772367581f);
+    r = fmaf(-k, 1.5707963705062866f, a);
+    r = fmaf(-k, -4.371138828673793e-08f, r);
+    r = fmaf(-k, -1.7763568394002505e-15f, r);
+    m = (int)k & 3;
+  } else {
+    const double k = rint((double)a * 0.63661977236758134308);
+    r = (float)fma(-k, 1.5707963267948966192, (double)a);
+    m = (int)(long long)k & 3;
+  }
   const float z = r * r;
   const float sp = r + r * z * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
   const float cp =
@@ -37,7 +46,6 @@ __device__ __forceinline__ void fast_sincosf(float a, float& s, float& c) {
   s = (m == 0) ? sp : (m == 1) ? cp : (m == 2) ? -sp : -cp;
   c = (m == 0) ? cp : (m == 1) ? -sp : (m == 2) ? -cp : sp;
 }
-
 __device__ __forceinline__ float act_f(int act, float a) {
   if (act == ACT_SINE) {
     float sv, cv;

@@ -1,0 +1,68 @@
+"""Two ranks (gloo, both on cuda:0) running the native throughput step
+(device Philox increments keyed by the GLOBAL path index, [grad|loss]
+all-reduce, replicated Adam) must reproduce the single-process step over the
+same global batch.  Needs a GPU; RCCL itself is exercised by the bench at N>1."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT, load_pkg
+
+pytestmark = pytest.mark.gpu
+D, M, N = 8, 64, 10
+LAYERS = [D + 1, 16, 16, 16, 16, 1]
+
+
+def _model(world, rank):
+    pkg = load_pkg()
+    torch.manual_seed(0)
+    Xi = np.array([1.0, 0.5] * (D // 2))[None, :]
+    m = pkg.BlackScholesBarenblatt(Xi, 1.0, M, N, D, LAYERS, "NAIS-Net", "Sine", device=torch.device("cuda:0"))
+    m.rank, m.world = rank, world
+    return m
+
+
+def _steps(m, k=3):
+    opt = m.new_optimizer_state()
+    losses = []
+    for it in range(k):
+        losses.append(float(m.device_step(opt, 1e-3, seed=it)))
+    torch.cuda.synchronize()
+    return m.params.cpu().numpy(), losses
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank,) + _steps(_model(world, rank)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_match_one_process():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    p1, l1 = _steps(_model(1, 0))
+    (_, pa, la), (_, pb, lb) = res
+    np.testing.assert_array_equal(pa, pb)                       # replicas identical
+    np.testing.assert_allclose(la, l1, rtol=1e-5)               # global loss = sum of shard losses
+    np.testing.assert_allclose(pa, p1, rtol=0, atol=2e-6)       # Adam steps agree
