@@ -10,7 +10,7 @@ import ctypes
 import os
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libdbsde.so")
+LIB_PATH = os.environ.get("DBSDE_LIB") or os.path.join(LIB_DIR, "libdbsde.so")  # DBSDE_LIB: A/B experiments only
 
 DBSDE_OK, DBSDE_EINVAL, DBSDE_EHIP, DBSDE_ENOMEM = 0, -1, -2, -3
 

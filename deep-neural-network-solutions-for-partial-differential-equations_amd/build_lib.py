@@ -8,11 +8,15 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", "engine.hip")]
-DEPS = SRC + [os.path.join(HERE, "csrc", "kernels.hpp"), os.path.join(ROOT, "include", "dbsde.h")]
+CSRC = os.path.join(HERE, "csrc")
+# translation units and their extra flags: the weight-gradient kernel is built
+# with VGPR-form MFMA (see csrc/tnw.hip); everything else with the defaults
+UNITS = [("engine.hip", []), ("tnw.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=true"])]
+DEPS = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith((".hip", ".hpp"))] + \
+    [os.path.join(ROOT, "include", "dbsde.h")]
 OUT = os.path.join(HERE, "lib", "libdbsde.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared", "-Wall"]
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-Wall"]
 
 
 def up_to_date():
@@ -27,13 +31,33 @@ def build(force=False, verbose=True):
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     tmp = OUT + ".tmp"
-    cmd = [HIPCC, *FLAGS, "-o", tmp, *SRC]
+    objdir = os.path.join(HERE, "lib", "obj")
+    os.makedirs(objdir, exist_ok=True)
+    cmds, objs = [], []
+    for src, extra in UNITS:
+        obj = os.path.join(objdir, src.replace(".hip", ".o"))
+        cmds.append([HIPCC, *FLAGS, *extra, "-c", "-o", obj, os.path.join(CSRC, src)])
+        objs.append(obj)
+    procs = []
+    for cmd in cmds:                       # the units compile in parallel
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    failed = False
+    for p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            sys.stderr.write(out)
+            failed = True
+    if failed:
+        raise RuntimeError("hipcc failed building libdbsde.so")
+    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:
-        print(" ".join(cmd), flush=True)
-    r = subprocess.run(cmd, capture_output=True, text=True)
+        print(" ".join(link), flush=True)
+    r = subprocess.run(link, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError("hipcc failed building libdbsde.so")
+        raise RuntimeError("hipcc failed linking libdbsde.so")
     os.replace(tmp, OUT)
     return OUT
 

@@ -24,6 +24,7 @@
 #include "../../include/dbsde.h"
 #include "kernels.hpp"
 #include "fused.hpp"
+#include "tnw.hpp"
 
 using namespace dbsde;
 
@@ -111,6 +112,11 @@ struct dbsde_ctx {
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
   int tn_splits = 96;              // weight-gradient GEMM row splits (A/B: 64..128 best on MI355X)
+  // wave-owned weight-gradient tiles (tnw.hpp): NAIS layouts with Dp == Wp
+  bool tnw = false;
+  int tnw_nb = 0, tnw_P = 0, tnw_S = 128;  // P * S = 1024 waves = one per SIMD at K = 3
+  float* slabW = nullptr;
+  int fin_blocks = 1;             // slabsum grid.x
 
   // ---- profiling
   bool prof = false;
@@ -427,57 +433,93 @@ int build_buffers(dbsde_ctx* c) {
   c->n_prep = (int)P.size();
 
   // ---- gradient slabs and finalize descriptors
-  c->slab.assign(K + 1, nullptr);
-  c->slab_mt.assign(K + 1, 0);
-  c->slab_nt.assign(K + 1, 0);
-  c->slab_mv.assign(K + 2, 0);
-  c->slab_nv.assign(K + 2, 0);
-  auto mkslab = [&](int j, int m, int n) -> int {
-    c->slab_mv[j] = m;
-    c->slab_nv[j] = n;
-    c->slab_mt[j] = (m + 63) / 64;
-    c->slab_nt[j] = (n + 63) / 64;
-    return dalloc_t(c, &c->slab[j], (size_t)c->tn_splits * c->slab_mt[j] * 64 * c->slab_nt[j] * 64);
-  };
-  c->slab.resize(K + 2, nullptr);
-  c->slab_mt.resize(K + 2, 0);
-  c->slab_nt.resize(K + 2, 0);
-  c->slab_mv.resize(K + 2, 0);
-  c->slab_nv.resize(K + 2, 0);
-  if ((rc = mkslab(0, c->Stot_x, Dp))) return rc;
-  for (int j = 1; j <= K; ++j)
-    if ((rc = mkslab(j, c->Wp[j], c->Wp[j - 1] + (c->has_v ? 0 : 1)))) return rc;
-  if ((rc = mkslab(K + 1, 16, c->Wp[K] + 1))) return rc;  // output layer: [w_out | b_out]
-
+  bool uniformW = true;
+  for (int j = 0; j <= K; ++j) uniformW = uniformW && c->Wp[j] == c->Wp[0];
+  // P = 2K + 2 problems in 4-wave workgroups: K odd
+  c->tnw = c->has_v && uniformW && c->Wp[0] == Dp && Dp <= 128 && K <= 6 && (2 * K + 2) % 4 == 0;
+  if (const char* e = getenv("DBSDE_TNW")) c->tnw = c->tnw && atoi(e) != 0;
+  if (const char* e = getenv("DBSDE_TNW_SPLITS")) c->tnw_S = std::max(8, std::min(1024, atoi(e) / 8 * 8));
   std::vector<PackDesc> F;
-  auto slabsum = [&](int j, int r0, int c0, int rows, int cols, float* dst, int dst_ld, float scale) {
-    const int ld = c->slab_nt[j] * 64;
-    PackDesc d = mk_desc(c->slab[j] + (size_t)r0 * ld + c0, ld, dst, dst_ld, rows, cols, 0, PK_SLABSUM, scale);
-    d.nslab = c->tn_splits;
-    d.slab_stride = (long long)c->slab_mt[j] * 64 * ld;
-    F.push_back(d);
-  };
-  slabsum(0, 0, 0, c->in.out, D + 1, gtag(c->in.w), D + 1, 1.f);
-  slabsum(0, 0, D + 1, c->in.out, 1, gtag(c->in.b), 1, 1.f);
-  if (c->has_v)
+  if (c->tnw) {
+    const int T = Dp, P = 2 * K + 2, S = c->tnw_S;
+    c->tnw_nb = T / 16;
+    c->tnw_P = P;
+    if ((rc = dalloc_t(c, &c->slabW, (size_t)S * P * T * T))) return rc;
+    auto wsum = [&](int p, int r0, int c0, int rows, int cols, float* dst, int dst_ld, float scale) {
+      PackDesc d = mk_desc(c->slabW + (size_t)p * T * T + (size_t)r0 * T + c0, T, dst, dst_ld, rows, cols, 0,
+                           PK_SLABSUM, scale);
+      d.nslab = S;
+      d.slab_stride = (long long)P * T * T;
+      F.push_back(d);
+    };
+    // x-stack problems p = j (input layer, V_j), block problems p = K + j (B_j)
+    wsum(0, 0, 0, c->in.out, D + 1, gtag(c->in.w), D + 1, 1.f);
+    wsum(0, 0, D + 1, c->in.out, 1, gtag(c->in.b), 1, 1.f);
     for (int j = 1; j <= K; ++j) {
       const Lin& v = c->V[j - 1];
-      slabsum(0, c->col[j], 0, v.out, D + 1, gtag(v.w), D + 1, 1.f);
-      slabsum(0, c->col[j], D + 1, v.out, 1, gtag(v.b), 1, 1.f);
-      slabsum(0, c->col[j], D + 1, v.out, 1, gtag(c->B[j - 1].b), 1, 1.f);
+      wsum(j, 0, 0, v.out, D + 1, gtag(v.w), D + 1, 1.f);
+      wsum(j, 0, D + 1, v.out, 1, gtag(v.b), 1, 1.f);
+      wsum(j, 0, D + 1, v.out, 1, gtag(c->B[j - 1].b), 1, 1.f);
+      const Lin& b = c->B[j - 1];
+      wsum(K + j, 0, 0, b.out, b.in, c->abar[j], LW, -1.f);  // Abar = -Bbar
     }
-  for (int j = 1; j <= K; ++j) {
-    const Lin& b = c->B[j - 1];
-    if (c->proj) {
-      slabsum(j, 0, 0, b.out, b.in, c->abar[j], LW, -1.f);  // Abar = -Bbar
-    } else {
-      slabsum(j, 0, 0, b.out, b.in, gtag(b.w), b.in, 1.f);
-      slabsum(j, 0, c->Wp[j - 1], b.out, 1, gtag(b.b), 1, 1.f);
+    // output layer: row 0 of problem 2K+1 is w_out, element (1, 0) is b_out
+    wsum(2 * K + 1, 0, 0, 1, c->out.in, gtag(c->out.w), 1, 1.f);
+    wsum(2 * K + 1, 1, 0, 1, 1, gtag(c->out.b), 1, 1.f);
+  } else {
+    c->slab.assign(K + 1, nullptr);
+    c->slab_mt.assign(K + 1, 0);
+    c->slab_nt.assign(K + 1, 0);
+    c->slab_mv.assign(K + 2, 0);
+    c->slab_nv.assign(K + 2, 0);
+    auto mkslab = [&](int j, int m, int n) -> int {
+      c->slab_mv[j] = m;
+      c->slab_nv[j] = n;
+      c->slab_mt[j] = (m + 63) / 64;
+      c->slab_nt[j] = (n + 63) / 64;
+      return dalloc_t(c, &c->slab[j], (size_t)c->tn_splits * c->slab_mt[j] * 64 * c->slab_nt[j] * 64);
+    };
+    c->slab.resize(K + 2, nullptr);
+    c->slab_mt.resize(K + 2, 0);
+    c->slab_nt.resize(K + 2, 0);
+    c->slab_mv.resize(K + 2, 0);
+    c->slab_nv.resize(K + 2, 0);
+    if ((rc = mkslab(0, c->Stot_x, Dp))) return rc;
+    for (int j = 1; j <= K; ++j)
+      if ((rc = mkslab(j, c->Wp[j], c->Wp[j - 1] + (c->has_v ? 0 : 1)))) return rc;
+    if ((rc = mkslab(K + 1, 16, c->Wp[K] + 1))) return rc;  // output layer: [w_out | b_out]
+
+    auto slabsum = [&](int j, int r0, int c0, int rows, int cols, float* dst, int dst_ld, float scale) {
+      const int ld = c->slab_nt[j] * 64;
+      PackDesc d = mk_desc(c->slab[j] + (size_t)r0 * ld + c0, ld, dst, dst_ld, rows, cols, 0, PK_SLABSUM, scale);
+      d.nslab = c->tn_splits;
+      d.slab_stride = (long long)c->slab_mt[j] * 64 * ld;
+      F.push_back(d);
+    };
+    slabsum(0, 0, 0, c->in.out, D + 1, gtag(c->in.w), D + 1, 1.f);
+    slabsum(0, 0, D + 1, c->in.out, 1, gtag(c->in.b), 1, 1.f);
+    if (c->has_v)
+      for (int j = 1; j <= K; ++j) {
+        const Lin& v = c->V[j - 1];
+        slabsum(0, c->col[j], 0, v.out, D + 1, gtag(v.w), D + 1, 1.f);
+        slabsum(0, c->col[j], D + 1, v.out, 1, gtag(v.b), 1, 1.f);
+        slabsum(0, c->col[j], D + 1, v.out, 1, gtag(c->B[j - 1].b), 1, 1.f);
+      }
+    for (int j = 1; j <= K; ++j) {
+      const Lin& b = c->B[j - 1];
+      if (c->proj) {
+        slabsum(j, 0, 0, b.out, b.in, c->abar[j], LW, -1.f);  // Abar = -Bbar
+      } else {
+        slabsum(j, 0, 0, b.out, b.in, gtag(b.w), b.in, 1.f);
+        slabsum(j, 0, c->Wp[j - 1], b.out, 1, gtag(b.b), 1, 1.f);
+      }
     }
+    slabsum(K + 1, 0, 0, 1, c->out.in, gtag(c->out.w), 1, 1.f);
+    slabsum(K + 1, 0, c->Wp[K], 1, 1, gtag(c->out.b), 1, 1.f);
   }
-  slabsum(K + 1, 0, 0, 1, c->out.in, gtag(c->out.w), 1, 1.f);
-  slabsum(K + 1, 0, c->Wp[K], 1, 1, gtag(c->out.b), 1, 1.f);
   c->n_fin = (int)F.size();
+  c->fin_blocks = 1;
+  for (const PackDesc& d : F) c->fin_blocks = std::max(c->fin_blocks, (d.rows * d.cols + 63) / 64);
   if ((rc = dalloc_t(c, &c->d_prep, P.size()))) return rc;
   if ((rc = dalloc_t(c, &c->d_fin, F.size()))) return rc;
   // descriptors are stored with tagged pointers; the kernel arguments carry the
@@ -741,9 +783,59 @@ int prep_weights(dbsde_ctx* c, const float* params) {
   return DBSDE_OK;
 }
 
+// Weight-gradient contraction, wave-owned tiles (tnw.hpp).  Problem p = j:
+// x-stack level j (alpha_j^T x + delta_j^T zbar); p = K + j: block B_j
+// (alpha_j^T h_{j-1} + delta_j^T hdot_{j-1}); plus the output-layer column sums.
+int launch_tnw(dbsde_ctx* c, int R, int Rp) {
+  const int K = c->K, S = c->Stot, T = c->Dp;
+  TNWArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int j = 0; j <= K; ++j) {
+    TNWProb& p = a.prob[j];
+    p.A1 = c->Alpha + c->col[j];
+    p.lda1 = S;
+    p.B1 = c->xin;
+    p.ldb1 = c->Dp;
+    p.A2 = c->Delta + c->col[j];
+    p.lda2 = S;
+    p.B2 = c->zbar;
+    p.ldb2 = c->Dp;
+  }
+  for (int j = 1; j <= K; ++j) {
+    TNWProb& p = a.prob[K + j];
+    p.A1 = c->Alpha + c->col[j];
+    p.lda1 = S;
+    p.B1 = c->H + c->col[j - 1];
+    p.ldb1 = S;
+    p.A2 = c->Delta + c->col[j];
+    p.lda2 = S;
+    p.B2 = c->Hdot + c->col[j - 1];
+    p.ldb2 = S;
+  }
+  a.P = c->tnw_P;
+  a.S = c->tnw_S;
+  a.nchunk = Rp / 16;
+  a.slab = c->slabW;
+  a.ubar = c->ubar;
+  a.Hk = c->H + c->col[K];
+  a.Hdk = c->Hdot + c->col[K];
+  a.ldh = S;
+  a.R = R;
+  if (Rp % 16 != 0 || c->Wp[K] != T || a.S % 8 != 0 || a.P != 2 * K + 2 || a.P % 4 != 0)
+    return fail(c, DBSDE_EINVAL, "internal: tnw geometry");
+  const double fl = 2.0 * 2.0 * (double)R * (K + 1) * c->L[1] * (c->D + 2) + 2.0 * 2.0 * (double)R * K * c->L[1] * c->L[1] +
+                    4.0 * (double)R * c->L[K + 1];
+  const unsigned grid = (unsigned)(a.S * a.P);
+  hipStream_t s = c->stream;
+  (void)grid;
+  if (c->tnw_nb < 1 || c->tnw_nb > 8) return fail(c, DBSDE_EINVAL, "internal: tnw tile");
+  RUN(c, "tn_weight_grad", fl, 0.0, (void)tnw_launch(c->tnw_nb, a, s));
+  return DBSDE_OK;
+}
+
 int finalize_grads(dbsde_ctx* c, const float* params, float* grad) {
   hipStream_t s = c->stream;
-  RUN(c, "grad_finalize", 0.0, 0.0, pack_tagged_kernel<<<dim3(64, c->n_fin), 256, 0, s>>>(c->d_fin, params, grad));
+  RUN(c, "grad_finalize", 0.0, 0.0, slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad));
   if (c->proj) {
     const int LW = c->L[1];
     const int nblk = (LW * LW + 255) / 256;
@@ -1164,6 +1256,10 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     }
     // ---- parameter gradients
     HIPC(c, hipMemsetAsync(grad, 0, (size_t)c->nparams * 4, s));
+    if (c->tnw) {
+      if ((rc = launch_tnw(c, R, Rp))) return rc;
+      if ((rc = finalize_grads(c, params, grad))) return rc;
+    } else {
     TNArgs ta;
     memset(&ta, 0, sizeof(ta));
     const int S_ = c->tn_splits;
@@ -1249,6 +1345,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
     RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
     if ((rc = finalize_grads(c, params, grad))) return rc;
+    }
   }
 
   if (out && (out->X || out->Y || out->Z)) {

@@ -759,4 +759,43 @@ __global__ void __launch_bounds__(256) netu_input_kernel(const float* t, const f
   xin[i] = v;
 }
 
+// grad[...] = scale * sum_k slab_k[...] for each PK_SLABSUM descriptor:
+// 64 elements per block, the slabs split over 4 thread groups whose fp64
+// partials are added in a fixed order.
+__global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, float* grad) {
+  const PackDesc& d = descs[blockIdx.y];
+  const int total = d.rows * d.cols;
+  if ((int)blockIdx.x * 64 >= total) return;
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  double s = 0.0;
+  int r = 0, cc = 0;
+  if (e < total) {
+    r = e / d.cols;
+    cc = e - r * d.cols;
+    const float* src = d.src + (size_t)r * d.src_ld + cc;
+    const int k0 = grp * d.nslab / 4, k1 = (grp + 1) * d.nslab / 4;
+    double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int k = k0;
+    for (; k + 8 <= k1; k += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sa[u] += src[(size_t)(k + u) * d.slab_stride];
+    }
+    for (; k < k1; ++k) sa[0] += src[(size_t)k * d.slab_stride];
+    s = ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7]));
+  }
+  __shared__ double part[4][64];
+  part[grp][lane] = s;
+  __syncthreads();
+  if (grp == 0 && e < total) {
+    const float v = d.scale * (float)((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
+    uintptr_t dv = (uintptr_t)d.dst;
+    float* dst = (dv & ((uintptr_t)1 << 61)) ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
+    if (d.transpose)
+      dst[(size_t)cc * d.dst_ld + r] = v;
+    else
+      dst[(size_t)r * d.dst_ld + cc] = v;
+  }
+}
+
 }  // namespace dbsde

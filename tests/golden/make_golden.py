@@ -217,9 +217,45 @@ def north_star(mods, seed=0, steps=(1, 3)):
     print(f"north_star loss={res['loss']:.6e} Y0={res['Y'][0, 0, 0]:.6f}")
 
 
+def north_star_trajectory(mods, seed=0, steps=(1, 10, 100)):
+    """G2b (SURVEY 8(d) accuracy): the reference DeepBSDE train() from the G2
+    init and batch stream; Y0 = net_u(0, Xi) after 1/10/100 Adam steps, plus
+    the parameters after 10 and 100 steps."""
+    import torch
+    D, M, N = 100, 1024, 50
+    layers = [D + 1] + 4 * [110] + [1]
+    Xi = np.array([1.0, 0.5] * (D // 2))[None, :]
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    with contextlib.redirect_stdout(io.StringIO()):
+        obj = mods["deep"].BlackScholesBarenblatt(Xi, 1.0, M, N, D, layers, "NAIS-Net", "Sine")
+    np.random.seed(1000 + seed)
+    out = dict(name="north_star_trajectory", seed=seed, batch_seed=1000 + seed, steps=np.array(steps))
+    y0 = []
+    done = 0
+    for s in steps:
+        with contextlib.redirect_stdout(io.StringIO()):
+            obj.train(s - done, 1e-3)
+        done = s
+        with torch.no_grad():
+            t0 = torch.zeros(1, 1)
+            x0 = torch.from_numpy(Xi).float()
+            u0 = obj.model(torch.cat([t0, x0], 1))
+        y0.append(float(u0))
+        if s >= 10:
+            out[f"params_after_{s}"] = _flat(obj.model.state_dict())
+        print(f"trajectory step {s}: Y0={y0[-1]:.6f}", flush=True)
+    out["Y0"] = np.array(y0)
+    np.savez_compressed(os.path.join(OUT, "g2_north_star_trajectory.npz"), **out)
+
+
 if __name__ == "__main__":
     m = _setup()
+    if "--trajectory-only" in sys.argv:
+        north_star_trajectory(m)
+        sys.exit(0)
     small_cases(m)
     train_cases(m)
     if "--skip-north-star" not in sys.argv:
         north_star(m)
+        north_star_trajectory(m)

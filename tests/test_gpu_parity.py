@@ -8,6 +8,7 @@ the reference's CPU BLAS):
   Y, Z                          abs 1e-4 * max(1, |ref|max)
   gradient                      abs 2e-4 * max|ref grad|
   parameters after 10 Adam steps abs 5e-5 ; north-star Y0 after 1/3 steps |dY0| < 1e-3
+  north-star Y0 = u(0, X0) after 1/10/100 reference train() steps   |dY0| < 1e-3  
 """
 import glob
 import os
@@ -51,20 +52,23 @@ def dev():
     return torch.device("cuda:0")
 
 
-def make_solver(pkg, dev, g, fused=True):
-    """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at create)."""
+def make_solver(pkg, dev, g, fused=True, tnw=True):
+    """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at
+    create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0)."""
     layers = [int(v) for v in g["layers"]]
     D = layers[0] - 1
-    old = os.environ.get("DBSDE_FUSED")
-    os.environ["DBSDE_FUSED"] = "1" if fused else "0"
+    env = {"DBSDE_FUSED": "1" if fused else "0", "DBSDE_TNW": "1" if tnw else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]), spec_for(pkg, str(g["problem"]), D),
                                 float(g["T"]), dev)
     finally:
-        if old is None:
-            del os.environ["DBSDE_FUSED"]
-        else:
-            os.environ["DBSDE_FUSED"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 def native_case(pkg, dev, g, want_grad=True, fused=True):
@@ -186,6 +190,27 @@ def test_north_star_shape(pkg, dev):
     assert abs(float(u_nat) - float(u_ref_params)) < 1e-3
 
 
+def test_north_star_trajectory_Y0(pkg, dev):
+    """SURVEY 8(d) accuracy: Y0 = u(0, X0) after 1, 10 and 100 steps of the
+    reference DeepBSDE train() (each call a fresh Adam, as in the reference),
+    from the reference's own init and numpy batch stream."""
+    g = _load(os.path.join(GOLDEN, "g2_north_star.npz"))
+    tr = _load(os.path.join(GOLDEN, "g2_north_star_trajectory.npz"))
+    layers = [int(v) for v in g["layers"]]
+    D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
+    m = pkg.BlackScholesBarenblatt(g["Xi"], float(g["T"]), M, N, D, layers, "NAIS-Net", "Sine", device=dev)
+    m.params.copy_(torch.from_numpy(g["params"]).to(dev))
+    np.random.seed(int(tr["batch_seed"]))
+    t0 = torch.zeros(1, device=dev)
+    x0 = torch.from_numpy(g["Xi"]).to(dev).reshape(1, D)
+    done = 0
+    for s, y0_ref in zip(tr["steps"], tr["Y0"]):
+        m.train(int(s) - done, 1e-3)
+        done = int(s)
+        u, _ = m.net_u(t0, x0)
+        assert abs(float(u) - float(y0_ref)) < 1e-3, (int(s), float(u), float(y0_ref))
+
+
 def test_net_u_matches_fixture_Y(pkg, dev):
     g = _load(G1[0])
     layers = [int(v) for v in g["layers"]]
@@ -204,8 +229,11 @@ def test_net_u_matches_fixture_Y(pkg, dev):
     np.testing.assert_allclose(du.cpu().numpy(), g["Z"].reshape(R, D), rtol=0, atol=1e-4)
 
 
-def test_fused_and_chain_paths_agree_at_north_star(pkg, dev):
-    """Both kernel paths on the full north-star batch (same params and W)."""
+@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False)], ids=["chain", "splitk_weight_grad"])
+def test_kernel_paths_agree_at_north_star(pkg, dev, variant):
+    """The default kernels (fused phases + wave-owned weight-gradient tiles)
+    against the per-layer chain path and against the split-K weight-gradient
+    GEMM, on the full north-star batch (same params and W)."""
     g = _load(os.path.join(GOLDEN, "g2_north_star.npz"))
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
@@ -213,8 +241,8 @@ def test_fused_and_chain_paths_agree_at_north_star(pkg, dev):
     W = np.cumsum(np.concatenate([np.zeros((M, 1, D)), np.sqrt(1 / N) * rs.normal(size=(M, N, D))], 1), 1)
     t = np.cumsum(np.concatenate([np.zeros((M, 1)), np.full((M, N), 1 / N)], 1), 1)
     res = []
-    for fused in (True, False):
-        s = make_solver(pkg, dev, g, fused)
+    for kw in ({}, variant):
+        s = make_solver(pkg, dev, g, **kw)
         params = torch.from_numpy(g["params"]).to(dev)
         grad, loss = torch.empty_like(params), torch.empty(1, device=dev)
         Y = torch.empty(M * (N + 1), device=dev)
