@@ -41,8 +41,9 @@ KERNEL_SYMBOL = {
     "gemm_xstack_fwd": "chain_gemm_kernel<7, 0>", "gemm_block_fwd": "chain_gemm_kernel<7, 1>",
     "gemm_block_inputgrad": "chain_gemm_kernel<7, 2>", "gemm_z_cotangent": "chain_gemm_kernel<7, 3>",
     "gemm_xstack_tangent": "chain_gemm_kernel<7, 4>", "gemm_block_tangent": "chain_gemm_kernel<7, 5>",
-    "gemm_block_reverse": "chain_gemm_kernel<7, 6>", "tn_weight_grad": "tn_gemm_kernel",
-    "rollout": "rollout_kernel",
+    "gemm_block_reverse": "chain_gemm_kernel<7, 6>", "tn_weight_grad": "tnw_kernel",
+    "fused_fwd_inputgrad": "phaseA_kernel", "fused_tangent_reverse": "phaseC_kernel",
+    "rollout": "rollout_kernel", "cotangent": "cotan_kernel", "grad_finalize": "slabsum_kernel",
 }
 
 
@@ -98,8 +99,8 @@ def traffic_from_pmc(symbol, launches_per_step):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)      # >= 50 steps after >= 10 warm-up
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--activation", default="Sine", help="experiments only; the headline is Sine")

@@ -105,14 +105,26 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
   }
 }
 
-__device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned long long offset,
-                                               uint32_t m, uint32_t n, uint32_t d) {
-  uint32_t c[4] = {d, n, m, (uint32_t)offset};
+// Four standard normals from one Philox4x32-10 block: both Box-Muller outputs
+// of the uniform pairs (c0, c1) and (c2, c3).  Counter = (d, n/4, m, offset),
+// key = seed: the stream is keyed by the global path index m, so sharding
+// paths over ranks reproduces the single-device increments.
+__device__ __forceinline__ void philox_normal4(unsigned long long seed, unsigned long long offset, uint32_t m,
+                                               uint32_t nq, uint32_t d, float z[4]) {
+  uint32_t c[4] = {d, nq, m, (uint32_t)offset};
   philox4x32_10(c, (uint32_t)seed ^ (uint32_t)(offset >> 32), (uint32_t)(seed >> 32));
-  // two uniforms in (0,1] -> one standard normal
-  float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);
-  float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);
-  return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+  const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
+  const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);            // [0, 1)
+  const float u3 = ((float)(c[2] >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  const float u4 = (float)(c[3] >> 8) * (1.0f / 16777216.0f);
+  const float r1 = sqrtf(-2.0f * logf(u1)), r2 = sqrtf(-2.0f * logf(u3));
+  float s1, c1, s2, c2;
+  sincospif(2.0f * u2, &s1, &c1);
+  sincospif(2.0f * u4, &s2, &c2);
+  z[0] = r1 * c1;
+  z[1] = r1 * s1;
+  z[2] = r2 * c2;
+  z[3] = r2 * s2;
 }
 
 // --------------------------------------------------------------------------
@@ -147,29 +159,47 @@ __global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
   float t0 = p.t ? p.t[(size_t)m * N1] : 0.0f;
   float w0 = p.W ? p.W[(size_t)m * N1 * p.D + d] : 0.0f;
   size_t r = (size_t)m * N1;
-  for (int n = 0; n < p.N; ++n, ++r) {
-    float* xr = p.xin + r * p.ldx;
-    xr[1 + d] = x;
-    if (d == 0) {
-      xr[0] = t0;
-      xr[p.D + 1] = 1.0f;
-    }
-    float t1, dw;
+  // blocks of 4 steps: the increments of a block (Philox, or the host W
+  // differences) are formed first, independent of x; then the sequential
+  // Euler-Maruyama updates
+  for (int n0 = 0; n0 < p.N; n0 += 4) {
+    float dw[4], t1[4];
     if (p.W) {
-      t1 = p.t[(size_t)m * N1 + n + 1];
-      float w1 = p.W[((size_t)m * N1 + n + 1) * p.D + d];
-      dw = __fsub_rn(w1, w0);
-      w0 = w1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int n = min(n0 + k + 1, p.N);
+        const float w1 = p.W[((size_t)m * N1 + n) * p.D + d];
+        t1[k] = p.t[(size_t)m * N1 + n];
+        dw[k] = __fsub_rn(w1, w0);
+        w0 = w1;
+      }
     } else {
-      t1 = p.t ? p.t[(size_t)m * N1 + n + 1] : (float)((double)p.T * (double)(n + 1) / (double)p.N);
-      dw = sqdt * philox_normal(p.seed, p.offset, (uint32_t)(p.path0 + m), (uint32_t)n, (uint32_t)d);
+      float z[4];
+      philox_normal4(p.seed, p.offset, (uint32_t)(p.path0 + m), (uint32_t)(n0 >> 2), (uint32_t)d, z);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int n = min(n0 + k + 1, p.N);
+        t1[k] = p.t ? p.t[(size_t)m * N1 + n] : (float)((double)p.T * (double)n / (double)p.N);
+        dw[k] = sqdt * z[k];
+      }
     }
-    const float dt = __fsub_rn(t1, t0);
-    const float sg = __fadd_rn(__fmul_rn(p.sig_a, x), p.sig_b);
-    const float s = __fmul_rn(sg, dw);
-    p.sdw[r * p.ldx + d] = s;
-    x = __fadd_rn(__fadd_rn(x, __fmul_rn(__fmul_rn(p.mu_a, x), dt)), s);
-    t0 = t1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (n0 + k >= p.N) break;
+      float* xr = p.xin + r * p.ldx;
+      xr[1 + d] = x;
+      if (d == 0) {
+        xr[0] = t0;
+        xr[p.D + 1] = 1.0f;
+      }
+      const float dt = __fsub_rn(t1[k], t0);
+      const float sg = __fadd_rn(__fmul_rn(p.sig_a, x), p.sig_b);
+      const float s = __fmul_rn(sg, dw[k]);
+      p.sdw[r * p.ldx + d] = s;
+      x = __fadd_rn(__fadd_rn(x, __fmul_rn(__fmul_rn(p.mu_a, x), dt)), s);
+      t0 = t1[k];
+      ++r;
+    }
   }
   float* xr = p.xin + r * p.ldx;  // n = N
   xr[1 + d] = x;
