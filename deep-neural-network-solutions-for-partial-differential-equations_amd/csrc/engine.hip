@@ -24,6 +24,7 @@
 #include "../../include/dbsde.h"
 #include "kernels.hpp"
 #include "fused.hpp"
+#include "phase.hpp"
 #include "tnw.hpp"
 
 using namespace dbsde;
@@ -111,6 +112,10 @@ struct dbsde_ctx {
 
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
+  bool phase_v1 = false;          // DBSDE_PHASE_V1=1: the LDS-relayout phase kernels (fused.hpp) instead of phase.hpp
+  // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
+  // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
+  std::vector<float*> imgX, imgZ, imgF, imgB;
   int tn_splits = 96;              // weight-gradient GEMM row splits (A/B: 64..128 best on MI355X)
   // wave-owned weight-gradient tiles (tnw.hpp): NAIS layouts with Dp == Wp
   bool tnw = false;
@@ -206,21 +211,17 @@ struct FusedVariant {
   int T, TD, K, act;
   void (*A)(FusedArgs);
   void (*C)(FusedArgs);
+  void (*A2)(FusedArgs);
+  void (*C2)(FusedArgs);
 };
+#define FV(T, TD, K, ACT)                                                                            \
+  {T, TD, K, ACT, phaseA_kernel<T, TD, K, ACT>, phaseC_kernel<T, TD, K, ACT>, phaseA2_kernel<T, TD, K, ACT>, \
+   phaseC2_kernel<T, TD, K, ACT>}
 const FusedVariant kFused[] = {
-    {7, 7, 3, 0, phaseA_kernel<7, 7, 3, 0>, phaseC_kernel<7, 7, 3, 0>},
-    {7, 7, 3, 1, phaseA_kernel<7, 7, 3, 1>, phaseC_kernel<7, 7, 3, 1>},
-    {7, 7, 3, 2, phaseA_kernel<7, 7, 3, 2>, phaseC_kernel<7, 7, 3, 2>},
-    {1, 1, 1, 0, phaseA_kernel<1, 1, 1, 0>, phaseC_kernel<1, 1, 1, 0>},
-    {1, 1, 1, 1, phaseA_kernel<1, 1, 1, 1>, phaseC_kernel<1, 1, 1, 1>},
-    {1, 1, 1, 2, phaseA_kernel<1, 1, 1, 2>, phaseC_kernel<1, 1, 1, 2>},
-    {1, 1, 2, 0, phaseA_kernel<1, 1, 2, 0>, phaseC_kernel<1, 1, 2, 0>},
-    {1, 1, 2, 1, phaseA_kernel<1, 1, 2, 1>, phaseC_kernel<1, 1, 2, 1>},
-    {1, 1, 2, 2, phaseA_kernel<1, 1, 2, 2>, phaseC_kernel<1, 1, 2, 2>},
-    {1, 1, 3, 0, phaseA_kernel<1, 1, 3, 0>, phaseC_kernel<1, 1, 3, 0>},
-    {1, 1, 3, 1, phaseA_kernel<1, 1, 3, 1>, phaseC_kernel<1, 1, 3, 1>},
-    {1, 1, 3, 2, phaseA_kernel<1, 1, 3, 2>, phaseC_kernel<1, 1, 3, 2>},
+    FV(7, 7, 3, 0), FV(7, 7, 3, 1), FV(7, 7, 3, 2), FV(1, 1, 1, 0), FV(1, 1, 1, 1), FV(1, 1, 1, 2),
+    FV(1, 1, 2, 0), FV(1, 1, 2, 1), FV(1, 1, 2, 2), FV(1, 1, 3, 0), FV(1, 1, 3, 1), FV(1, 1, 3, 2),
 };
+#undef FV
 int fused_variant(int T, int TD, int K, int act) {
   for (int i = 0; i < (int)(sizeof(kFused) / sizeof(kFused[0])); ++i)
     if (kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act) return i;
@@ -322,6 +323,8 @@ int build_net(dbsde_ctx* c) {
   const char* env = getenv("DBSDE_FUSED");
   const bool allow = !(env && env[0] == '0');
   c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act) >= 0;
+  const char* v1 = getenv("DBSDE_PHASE_V1");
+  c->phase_v1 = v1 && v1[0] == '1';
   return DBSDE_OK;
 }
 
@@ -395,20 +398,45 @@ int build_buffers(dbsde_ctx* c) {
   c->opt_nparts = 256;
   if ((rc = dalloc_t(c, &c->opt_part, c->opt_nparts))) return rc;
 
+  // ---- fragment images for the phase kernels (phase.hpp)
+  const int TW = c->Wp[0] / 16, TDp = Dp / 16;
+  c->imgX.assign(K + 1, nullptr);
+  c->imgZ.assign(K + 1, nullptr);
+  c->imgF.assign(K + 1, nullptr);
+  c->imgB.assign(K + 1, nullptr);
+  if (c->fused) {
+    for (int j = 0; j <= (c->has_v ? K : 0); ++j) {
+      if ((rc = dalloc_t(c, &c->imgX[j], (size_t)TW * TDp * 256))) return rc;
+      if ((rc = dalloc_t(c, &c->imgZ[j], (size_t)TW * TDp * 256))) return rc;
+    }
+    for (int j = 1; j <= K; ++j) {
+      if ((rc = dalloc_t(c, &c->imgF[j], (size_t)TW * TW * 256))) return rc;
+      if ((rc = dalloc_t(c, &c->imgB[j], (size_t)TW * TW * 256))) return rc;
+    }
+  }
+  auto frag = [](PackDesc d, float* img, int tin, int row0, int col0) {
+    d.fdst = img;
+    d.ftin = tin;
+    d.frow0 = row0;
+    d.fcol0 = col0;
+    return d;
+  };
+
   // ---- prep descriptors: flat params -> packed weight buffers
   std::vector<PackDesc> P;
   auto add_x_level = [&](int j, const Lin& w, const Lin* b2) {
     float* dst = c->BtIn + (size_t)c->col[j] * Dp;
-    P.push_back(mk_desc(ptag(w.w), D + 1, dst, Dp, w.out, D + 1, 0, PK_COPY));
+    P.push_back(frag(mk_desc(ptag(w.w), D + 1, dst, Dp, w.out, D + 1, 0, PK_COPY), c->imgX[j], TDp, 0, 0));
     if (b2) {
       PackDesc d = mk_desc(ptag(w.b), 1, dst + D + 1, Dp, w.out, 1, 0, PK_ADD2);
       d.src2 = ptag(b2->b);
       d.src2_ld = 1;
-      P.push_back(d);
+      P.push_back(frag(d, c->imgX[j], TDp, 0, D + 1));
     } else {
-      P.push_back(mk_desc(ptag(w.b), 1, dst + D + 1, Dp, w.out, 1, 0, PK_COPY));
+      P.push_back(frag(mk_desc(ptag(w.b), 1, dst + D + 1, Dp, w.out, 1, 0, PK_COPY), c->imgX[j], TDp, 0, D + 1));
     }
-    P.push_back(mk_desc(ptag(w.w), D + 1, c->BtZ + c->col[j], c->Stot_x, w.out, D + 1, 1, PK_COPY));
+    P.push_back(frag(mk_desc(ptag(w.w), D + 1, c->BtZ + c->col[j], c->Stot_x, w.out, D + 1, 1, PK_COPY), c->imgZ[j],
+                     TW, 0, 0));
   };
   add_x_level(0, c->in, nullptr);
   if (c->has_v)
@@ -418,13 +446,15 @@ int build_buffers(dbsde_ctx* c) {
     if (c->proj) {
       PackDesc d = mk_desc(c->rtr[j], LW, c->Bf[j], c->Wp[j - 1], LW, LW, 0, PK_NEGPROJ);
       d.proj = c->norms + (j - 1);
-      P.push_back(d);
+      P.push_back(frag(d, c->imgF[j], TW, 0, 0));
       d = mk_desc(c->rtr[j], LW, c->Bb[j], c->Wp[j], LW, LW, 1, PK_NEGPROJ);
       d.proj = c->norms + (j - 1);
-      P.push_back(d);
+      P.push_back(frag(d, c->imgB[j], TW, 0, 0));
     } else {
-      P.push_back(mk_desc(ptag(b.w), b.in, c->Bf[j], c->Wp[j - 1], b.out, b.in, 0, PK_COPY));
-      P.push_back(mk_desc(ptag(b.w), b.in, c->Bb[j], c->Wp[j], b.out, b.in, 1, PK_COPY));
+      P.push_back(frag(mk_desc(ptag(b.w), b.in, c->Bf[j], c->Wp[j - 1], b.out, b.in, 0, PK_COPY), c->imgF[j], TW,
+                       0, 0));
+      P.push_back(frag(mk_desc(ptag(b.w), b.in, c->Bb[j], c->Wp[j], b.out, b.in, 1, PK_COPY), c->imgB[j], TW, 0,
+                       0));
       P.push_back(mk_desc(ptag(b.b), 1, c->beta[j], 1, b.out, 1, 0, PK_COPY));
     }
   }
@@ -662,6 +692,10 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
       d.dst[(size_t)cc * d.dst_ld + r] = v;
     else
       d.dst[(size_t)r * d.dst_ld + cc] = v;
+    if (d.fdst) {
+      const int dr = (d.transpose ? cc : r) + d.frow0, dc = (d.transpose ? r : cc) + d.fcol0;
+      d.fdst[frag_off(dr, dc, d.ftin)] = v;
+    }
   }
 }
 // Small LDS-tiled SGEMM for the L x L NAIS matrices (L <= 128): one 16x16
@@ -994,6 +1028,26 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int N1) {
   a.ubar = c->ubar;
   a.Hdot = c->Hdot;
   a.Alpha = c->Alpha;
+  // stage sequences of phaseA2 / phaseC2 (phase.hpp)
+  const int TW = c->Wp[0] / 16, TDp = c->Dp / 16, K = c->K;
+  auto addA = [&](const float* img, int nf) { a.simgA[a.nA] = img; a.snfA[a.nA++] = nf; };
+  auto addC = [&](const float* img, int nf) { a.simgC[a.nC] = img; a.snfC[a.nC++] = nf; };
+  addA(c->imgX[0], TW * TDp);
+  addC(c->imgX[0], TW * TDp);
+  for (int j = 1; j <= K; ++j) {
+    addA(c->imgF[j], TW * TW);
+    addC(c->imgF[j], TW * TW);
+    if (c->has_v) {
+      addA(c->imgX[j], TW * TDp);
+      addC(c->imgX[j], TW * TDp);
+    }
+  }
+  for (int j = K; j >= 1; --j) {
+    if (c->has_v) addA(c->imgZ[j], TW * TDp);
+    addA(c->imgB[j], TW * TW);
+    addC(c->imgB[j], TW * TW);
+  }
+  addA(c->imgZ[0], TW * TDp);
   return a;
 }
 
@@ -1070,7 +1124,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   if (rc) return rc;
   HIPC(c, hipSetDevice(c->device));
   const int M = b->M, N = b->N, N1 = N + 1, D = c->D, K = c->K, S = c->Stot;
-  const int R = M * N1, Rp = (R + CH_BM - 1) / CH_BM * CH_BM;
+  const int R = M * N1, Rp = (R + PH_ROWS - 1) / PH_ROWS * PH_ROWS;
   if ((rc = ensure_rows(c, Rp, N))) return rc;
   hipStream_t s = c->stream;
   const auto& L = c->L;
@@ -1113,8 +1167,12 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     fa = fused_args(c, R, N1);
     const int nv = nv_x(c);
     const double flA = 2.0 * R * ((D + 1.0) * nv + 2.0 * K * L[1] * (double)L[1] + (double)nv * D);
-    RUN(c, "fused_fwd_inputgrad", flA, 4.0 * R * (c->Dp + 4.0 * S + 8.0),
-        kFused[fv].A<<<Rp / 64, 256, 0, s>>>(fa));
+    if (c->phase_v1)
+      RUN(c, "fused_fwd_inputgrad", flA, 4.0 * R * (c->Dp + 4.0 * S + 8.0),
+          kFused[fv].A<<<Rp / 64, 256, 0, s>>>(fa));
+    else
+      RUN(c, "fused_fwd_inputgrad", flA, 4.0 * R * (c->Dp + 4.0 * S + 8.0),
+          kFused[fv].A2<<<Rp / PH_ROWS, 64 * PH_WAVES, 0, s>>>(fa));
     CotanArgs ca{};
     ca.R = R;
     ca.Rp = Rp;
@@ -1178,7 +1236,11 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     if (fv >= 0) {
       const int nv = nv_x(c);
       const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
-      RUN(c, "fused_tangent_reverse", flC, 4.0 * R * (c->Dp + 5.0 * S), kFused[fv].C<<<Rp / 64, 256, 0, s>>>(fa));
+      if (c->phase_v1)
+        RUN(c, "fused_tangent_reverse", flC, 4.0 * R * (c->Dp + 5.0 * S), kFused[fv].C<<<Rp / 64, 256, 0, s>>>(fa));
+      else
+        RUN(c, "fused_tangent_reverse", flC, 4.0 * R * (c->Dp + 5.0 * S),
+            kFused[fv].C2<<<Rp / PH_ROWS, 64 * PH_WAVES, 0, s>>>(fa));
     } else {
       // ---- forward tangent along zbar
       {
@@ -1361,7 +1423,7 @@ int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const 
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
   if (!params || !t || !X || R < 1) return fail(c, DBSDE_EINVAL, "bad net_u arguments");
   HIPC(c, hipSetDevice(c->device));
-  const int Rp = (R + CH_BM - 1) / CH_BM * CH_BM, D = c->D;
+  const int Rp = (R + PH_ROWS - 1) / PH_ROWS * PH_ROWS, D = c->D;
   int rc;
   if ((rc = ensure_rows(c, Rp, 1))) return rc;
   hipStream_t s = c->stream;

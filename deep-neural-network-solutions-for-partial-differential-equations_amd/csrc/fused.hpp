@@ -40,6 +40,13 @@ struct FusedArgs {
   const float* zbar;        // [Rp, Dp]
   const float* ubar;        // [Rp]
   float *Hdot, *Alpha;
+  // phase.hpp kernels: fragment images of the stage sequence of each pass
+  const float* simgA[32];
+  int snfA[32];
+  int nA;
+  const float* simgC[32];
+  int snfC[32];
+  int nC;
 };
 
 template <int TT>
@@ -380,7 +387,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
       const float zv = z.v[t][jj];
       if (c >= 1 && c <= D) {
         const float xv = Xl[(4 * q + jj) * LDX + c];
-        s_zs += zv * sr[c - 1];
+        s_zs += zv * sr[c];
         s_xz += xv * zv;
         s_zz += zv * zv;
         s_x += xv;
@@ -574,7 +581,7 @@ __global__ void __launch_bounds__(256) cotan_kernel(CotanArgs p) {
           const float xv = xr[c], zv = zr[c];
           if (!term) {
             const float dphidz = -p.phi_r * p.phi_c * xv + 2.f * p.phi_zz * zv;
-            const float sd = p.q3S ? p.q3S[n] : sr[c - 1];
+            const float sd = p.q3S ? p.q3S[n] : sr[c];
             v = coefY * (dphidz * dt + sd);
           } else {
             const float dg = (p.g_kind == 0) ? 2.f * xv : (p.g_kind == 3 ? xv * gsc : gsc);

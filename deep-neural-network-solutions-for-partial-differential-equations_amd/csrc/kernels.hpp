@@ -145,7 +145,7 @@ struct RolloutArgs {
   long long path0;
   float mu_a, sig_a, sig_b;
   float* xin;       // [Rp, ldx]
-  float* sdw;       // [Rp, ldx]   (cols 0..D-1)
+  float* sdw;       // [Rp, ldx]   (cols 1..D, aligned with X in xin)
 };
 
 __global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
       const float dt = __fsub_rn(t1[k], t0);
       const float sg = __fadd_rn(__fmul_rn(p.sig_a, x), p.sig_b);
       const float s = __fmul_rn(sg, dw[k]);
-      p.sdw[r * p.ldx + d] = s;
+      p.sdw[r * p.ldx + 1 + d] = s;
       x = __fadd_rn(__fadd_rn(x, __fmul_rn(__fmul_rn(p.mu_a, x), dt)), s);
       t0 = t1[k];
       ++r;
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
   }
   float* xr = p.xin + r * p.ldx;  // n = N
   xr[1 + d] = x;
-  p.sdw[r * p.ldx + d] = 0.0f;
+  p.sdw[r * p.ldx + 1 + d] = 0.0f;
   if (d == 0) {
     xr[0] = t0;
     xr[p.D + 1] = 1.0f;
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(256) q3_sum_kernel(const float* sdw, int ldx, 
   const int n = blockIdx.x;
   __shared__ float red[256];
   float acc = 0.f;
-  for (int m = threadIdx.x; m < M; m += 256) acc += sdw[((size_t)m * (N + 1) + n) * ldx];
+  for (int m = threadIdx.x; m < M; m += 256) acc += sdw[((size_t)m * (N + 1) + n) * ldx + 1];
   red[threadIdx.x] = acc;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
         const float z = acc[t][j];
         if (c >= 1 && c <= D) {
           const float xv = xr[c];
-          s_zs += z * sr[c - 1];
+          s_zs += z * sr[c];
           s_xz += xv * z;
           s_zz += z * z;
           s_x += xv;
@@ -432,7 +432,7 @@ __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
           const float xv = xr[c];
           if (!term) {
             const float dphidz = -p.phi_r * p.phi_c * xv + 2.f * p.phi_zz * z;
-            const float sd = p.q3S ? S : sr[c - 1];
+            const float sd = p.q3S ? S : sr[c];
             zb = coefY * (dphidz * dt + sd);
           } else {
             const float dg = (p.g_kind == 0) ? 2.f * xv : (p.g_kind == 3 ? xv * gsc : gsc);
@@ -695,7 +695,17 @@ struct PackDesc {
   int nslab;           // PK_SLABSUM: slabs of stride slab_stride
   long long slab_stride;
   const double* proj;  // PK_NEGPROJ: [norm, ...] of this block
+  // optional second destination: an MFMA fragment image (phase.hpp) of the
+  // logical [out][in] matrix, element (dr + frow0, dc + fcol0) with
+  // (dr, dc) = transpose ? (c, r) : (r, c); ftin = 16-col input blocks
+  float* fdst;
+  int ftin, frow0, fcol0;
 };
+// float offset of W[o][i] in a fragment image with tin input blocks:
+// fragment (o/16, i/16), lane (o%16) + 16 ((i/4)%4), component i%4
+__host__ __device__ __forceinline__ long long frag_off(int o, int i, int tin) {
+  return ((((long long)(o >> 4) * tin + (i >> 4)) * 64 + (o & 15) + 16 * ((i >> 2) & 3)) << 2) + (i & 3);
+}
 
 // --------------------------------------------------------------------------
 // clip_grad_norm_ + Adam/AdamW/SGD (nd_BSPDE_case.py:383-384; torch defaults)
