@@ -36,13 +36,15 @@ LR = 1e-3
 U0_EXACT = float(np.exp((0.05 + 0.4 ** 2) * 1.0) * 62.5)     # DeepBSDE.py:345-349 at Xi=[1,.5]*50
 PEAK_FP32_MFMA_TFLOPS = 157.3                                # MI355X_MICROARCH.md, dense f32 MFMA
 PEAK_HBM_GBS = 8000.0
+# rocprof symbol suffix of the phase kernels the library launches (DBSDE_PHASE, default 3)
+PHASE_SUFFIX = {"1": "", "2": "2"}.get(os.environ.get("DBSDE_PHASE", "3"), "3")
 # rocprof symbol of each profiled launch class (EPI ids from csrc/kernels.hpp)
 KERNEL_SYMBOL = {
     "gemm_xstack_fwd": "chain_gemm_kernel<7, 0>", "gemm_block_fwd": "chain_gemm_kernel<7, 1>",
     "gemm_block_inputgrad": "chain_gemm_kernel<7, 2>", "gemm_z_cotangent": "chain_gemm_kernel<7, 3>",
     "gemm_xstack_tangent": "chain_gemm_kernel<7, 4>", "gemm_block_tangent": "chain_gemm_kernel<7, 5>",
     "gemm_block_reverse": "chain_gemm_kernel<7, 6>", "tn_weight_grad": "tnw_kernel",
-    "fused_fwd_inputgrad": "phaseA_kernel", "fused_tangent_reverse": "phaseC_kernel",
+    "fused_fwd_inputgrad": f"phaseA{PHASE_SUFFIX}_kernel", "fused_tangent_reverse": f"phaseC{PHASE_SUFFIX}_kernel",
     "rollout": "rollout_kernel", "cotangent": "cotan_kernel", "grad_finalize": "slabsum_kernel",
 }
 

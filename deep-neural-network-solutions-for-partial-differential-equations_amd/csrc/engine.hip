@@ -25,6 +25,7 @@
 #include "kernels.hpp"
 #include "fused.hpp"
 #include "phase.hpp"
+#include "phase3.hpp"
 #include "tnw.hpp"
 
 using namespace dbsde;
@@ -112,7 +113,7 @@ struct dbsde_ctx {
 
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
-  bool phase_v1 = false;          // DBSDE_PHASE_V1=1: the LDS-relayout phase kernels (fused.hpp) instead of phase.hpp
+  int phase_ver = 3;              // DBSDE_PHASE=1|2|3: fused.hpp (LDS relayout) / phase.hpp (8-wave) / phase3.hpp (4-wave)
   // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
   // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
   std::vector<float*> imgX, imgZ, imgF, imgB;
@@ -213,10 +214,12 @@ struct FusedVariant {
   void (*C)(FusedArgs);
   void (*A2)(FusedArgs);
   void (*C2)(FusedArgs);
+  void (*A3)(FusedArgs);
+  void (*C3)(FusedArgs);
 };
 #define FV(T, TD, K, ACT)                                                                            \
   {T, TD, K, ACT, phaseA_kernel<T, TD, K, ACT>, phaseC_kernel<T, TD, K, ACT>, phaseA2_kernel<T, TD, K, ACT>, \
-   phaseC2_kernel<T, TD, K, ACT>}
+   phaseC2_kernel<T, TD, K, ACT>, phaseA3_kernel<T, TD, K, ACT>, phaseC3_kernel<T, TD, K, ACT>}
 const FusedVariant kFused[] = {
     FV(7, 7, 3, 0), FV(7, 7, 3, 1), FV(7, 7, 3, 2), FV(1, 1, 1, 0), FV(1, 1, 1, 1), FV(1, 1, 1, 2),
     FV(1, 1, 2, 0), FV(1, 1, 2, 1), FV(1, 1, 2, 2), FV(1, 1, 3, 0), FV(1, 1, 3, 1), FV(1, 1, 3, 2),
@@ -323,8 +326,8 @@ int build_net(dbsde_ctx* c) {
   const char* env = getenv("DBSDE_FUSED");
   const bool allow = !(env && env[0] == '0');
   c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act) >= 0;
-  const char* v1 = getenv("DBSDE_PHASE_V1");
-  c->phase_v1 = v1 && v1[0] == '1';
+  const char* pv = getenv("DBSDE_PHASE");
+  c->phase_ver = pv ? std::max(1, std::min(3, atoi(pv))) : 3;
   return DBSDE_OK;
 }
 
@@ -414,9 +417,11 @@ int build_buffers(dbsde_ctx* c) {
       if ((rc = dalloc_t(c, &c->imgB[j], (size_t)TW * TW * 256))) return rc;
     }
   }
-  auto frag = [](PackDesc d, float* img, int tin, int row0, int col0) {
+  const bool tmajor = c->phase_ver == 3;
+  auto frag = [tmajor](PackDesc d, float* img, int tin, int tout, int row0, int col0) {
     d.fdst = img;
     d.ftin = tin;
+    d.ftout = tmajor ? tout : 0;
     d.frow0 = row0;
     d.fcol0 = col0;
     return d;
@@ -426,17 +431,17 @@ int build_buffers(dbsde_ctx* c) {
   std::vector<PackDesc> P;
   auto add_x_level = [&](int j, const Lin& w, const Lin* b2) {
     float* dst = c->BtIn + (size_t)c->col[j] * Dp;
-    P.push_back(frag(mk_desc(ptag(w.w), D + 1, dst, Dp, w.out, D + 1, 0, PK_COPY), c->imgX[j], TDp, 0, 0));
+    P.push_back(frag(mk_desc(ptag(w.w), D + 1, dst, Dp, w.out, D + 1, 0, PK_COPY), c->imgX[j], TDp, TW, 0, 0));
     if (b2) {
       PackDesc d = mk_desc(ptag(w.b), 1, dst + D + 1, Dp, w.out, 1, 0, PK_ADD2);
       d.src2 = ptag(b2->b);
       d.src2_ld = 1;
-      P.push_back(frag(d, c->imgX[j], TDp, 0, D + 1));
+      P.push_back(frag(d, c->imgX[j], TDp, TW, 0, D + 1));
     } else {
-      P.push_back(frag(mk_desc(ptag(w.b), 1, dst + D + 1, Dp, w.out, 1, 0, PK_COPY), c->imgX[j], TDp, 0, D + 1));
+      P.push_back(frag(mk_desc(ptag(w.b), 1, dst + D + 1, Dp, w.out, 1, 0, PK_COPY), c->imgX[j], TDp, TW, 0, D + 1));
     }
     P.push_back(frag(mk_desc(ptag(w.w), D + 1, c->BtZ + c->col[j], c->Stot_x, w.out, D + 1, 1, PK_COPY), c->imgZ[j],
-                     TW, 0, 0));
+                     TW, TDp, 0, 0));
   };
   add_x_level(0, c->in, nullptr);
   if (c->has_v)
@@ -446,14 +451,14 @@ int build_buffers(dbsde_ctx* c) {
     if (c->proj) {
       PackDesc d = mk_desc(c->rtr[j], LW, c->Bf[j], c->Wp[j - 1], LW, LW, 0, PK_NEGPROJ);
       d.proj = c->norms + (j - 1);
-      P.push_back(frag(d, c->imgF[j], TW, 0, 0));
+      P.push_back(frag(d, c->imgF[j], TW, TW, 0, 0));
       d = mk_desc(c->rtr[j], LW, c->Bb[j], c->Wp[j], LW, LW, 1, PK_NEGPROJ);
       d.proj = c->norms + (j - 1);
-      P.push_back(frag(d, c->imgB[j], TW, 0, 0));
+      P.push_back(frag(d, c->imgB[j], TW, TW, 0, 0));
     } else {
       P.push_back(frag(mk_desc(ptag(b.w), b.in, c->Bf[j], c->Wp[j - 1], b.out, b.in, 0, PK_COPY), c->imgF[j], TW,
-                       0, 0));
-      P.push_back(frag(mk_desc(ptag(b.w), b.in, c->Bb[j], c->Wp[j], b.out, b.in, 1, PK_COPY), c->imgB[j], TW, 0,
+                       TW, 0, 0));
+      P.push_back(frag(mk_desc(ptag(b.w), b.in, c->Bb[j], c->Wp[j], b.out, b.in, 1, PK_COPY), c->imgB[j], TW, TW, 0,
                        0));
       P.push_back(mk_desc(ptag(b.b), 1, c->beta[j], 1, b.out, 1, 0, PK_COPY));
     }
@@ -694,7 +699,7 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
       d.dst[(size_t)r * d.dst_ld + cc] = v;
     if (d.fdst) {
       const int dr = (d.transpose ? cc : r) + d.frow0, dc = (d.transpose ? r : cc) + d.fcol0;
-      d.fdst[frag_off(dr, dc, d.ftin)] = v;
+      d.fdst[frag_off(dr, dc, d.ftin, d.ftout)] = v;
     }
   }
 }
@@ -999,6 +1004,7 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int N1) {
   a.R = R;
   a.N1 = N1;
   a.D = c->D;
+  a.gcols = c->D;
   a.Dp = c->Dp;
   a.W = c->Wp[0];
   a.S = c->Stot;
@@ -1030,24 +1036,38 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int N1) {
   a.Alpha = c->Alpha;
   // stage sequences of phaseA2 / phaseC2 (phase.hpp)
   const int TW = c->Wp[0] / 16, TDp = c->Dp / 16, K = c->K;
-  auto addA = [&](const float* img, int nf) { a.simgA[a.nA] = img; a.snfA[a.nA++] = nf; };
-  auto addC = [&](const float* img, int nf) { a.simgC[a.nC] = img; a.snfC[a.nC++] = nf; };
-  addA(c->imgX[0], TW * TDp);
-  addC(c->imgX[0], TW * TDp);
+  // phase3 streams every image as two pieces (input blocks [0, H) and [H, TI))
+  const bool pieces = c->phase_ver == 3;
+  auto add = [&](const float** imgs, int* nfs, int& n, const float* img, int TO, int TI) {
+    if (!pieces || TI < 2) {
+      imgs[n] = img;
+      nfs[n++] = TO * TI;
+      return;
+    }
+    const int H = (TI + 1) / 2;
+    imgs[n] = img;
+    nfs[n++] = H * TO;
+    imgs[n] = img + (size_t)H * TO * 256;
+    nfs[n++] = (TI - H) * TO;
+  };
+  auto addA = [&](const float* img, int TO, int TI) { add(a.simgA, a.snfA, a.nA, img, TO, TI); };
+  auto addC = [&](const float* img, int TO, int TI) { add(a.simgC, a.snfC, a.nC, img, TO, TI); };
+  addA(c->imgX[0], TW, TDp);
+  addC(c->imgX[0], TW, TDp);
   for (int j = 1; j <= K; ++j) {
-    addA(c->imgF[j], TW * TW);
-    addC(c->imgF[j], TW * TW);
+    addA(c->imgF[j], TW, TW);
+    addC(c->imgF[j], TW, TW);
     if (c->has_v) {
-      addA(c->imgX[j], TW * TDp);
-      addC(c->imgX[j], TW * TDp);
+      addA(c->imgX[j], TW, TDp);
+      addC(c->imgX[j], TW, TDp);
     }
   }
   for (int j = K; j >= 1; --j) {
-    if (c->has_v) addA(c->imgZ[j], TW * TDp);
-    addA(c->imgB[j], TW * TW);
-    addC(c->imgB[j], TW * TW);
+    if (c->has_v) addA(c->imgZ[j], TDp, TW);
+    addA(c->imgB[j], TW, TW);
+    addC(c->imgB[j], TW, TW);
   }
-  addA(c->imgZ[0], TW * TDp);
+  addA(c->imgZ[0], TDp, TW);
   return a;
 }
 
@@ -1167,12 +1187,13 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     fa = fused_args(c, R, N1);
     const int nv = nv_x(c);
     const double flA = 2.0 * R * ((D + 1.0) * nv + 2.0 * K * L[1] * (double)L[1] + (double)nv * D);
-    if (c->phase_v1)
-      RUN(c, "fused_fwd_inputgrad", flA, 4.0 * R * (c->Dp + 4.0 * S + 8.0),
-          kFused[fv].A<<<Rp / 64, 256, 0, s>>>(fa));
+    const double byA = 4.0 * R * (c->Dp + 4.0 * S + 8.0);
+    if (c->phase_ver == 1)
+      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / 64, 256, 0, s>>>(fa));
+    else if (c->phase_ver == 2)
+      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A2<<<Rp / PH_ROWS, 64 * PH_WAVES, 0, s>>>(fa));
     else
-      RUN(c, "fused_fwd_inputgrad", flA, 4.0 * R * (c->Dp + 4.0 * S + 8.0),
-          kFused[fv].A2<<<Rp / PH_ROWS, 64 * PH_WAVES, 0, s>>>(fa));
+      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A3<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
     CotanArgs ca{};
     ca.R = R;
     ca.Rp = Rp;
@@ -1236,11 +1257,13 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     if (fv >= 0) {
       const int nv = nv_x(c);
       const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
-      if (c->phase_v1)
-        RUN(c, "fused_tangent_reverse", flC, 4.0 * R * (c->Dp + 5.0 * S), kFused[fv].C<<<Rp / 64, 256, 0, s>>>(fa));
+      const double byC = 4.0 * R * (c->Dp + 5.0 * S);
+      if (c->phase_ver == 1)
+        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / 64, 256, 0, s>>>(fa));
+      else if (c->phase_ver == 2)
+        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C2<<<Rp / PH_ROWS, 64 * PH_WAVES, 0, s>>>(fa));
       else
-        RUN(c, "fused_tangent_reverse", flC, 4.0 * R * (c->Dp + 5.0 * S),
-            kFused[fv].C2<<<Rp / PH_ROWS, 64 * PH_WAVES, 0, s>>>(fa));
+        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C3<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
     } else {
       // ---- forward tangent along zbar
       {

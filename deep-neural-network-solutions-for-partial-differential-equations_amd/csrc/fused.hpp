@@ -23,6 +23,7 @@ namespace dbsde {
 struct FusedArgs {
   int R, N1, D, Dp, W, S;   // rows, N+1, D, padded D, padded level width, level stride
   int has_v, act;
+  int gcols;                // leading state columns entering g (row sums s_x, s_xx)
   float rho;
   const float* xin;         // [Rp, Dp]
   const float* BtIn;        // [Stot_x, Dp]

@@ -700,11 +700,14 @@ struct PackDesc {
   // (dr, dc) = transpose ? (c, r) : (r, c); ftin = 16-col input blocks
   float* fdst;
   int ftin, frow0, fcol0;
+  int ftout;           // > 0: t-major image (phase3.hpp), fragment (o, t) at t * ftout + o
 };
-// float offset of W[o][i] in a fragment image with tin input blocks:
-// fragment (o/16, i/16), lane (o%16) + 16 ((i/4)%4), component i%4
-__host__ __device__ __forceinline__ long long frag_off(int o, int i, int tin) {
-  return ((((long long)(o >> 4) * tin + (i >> 4)) * 64 + (o & 15) + 16 * ((i >> 2) & 3)) << 2) + (i & 3);
+// float offset of W[o][i] in a fragment image with tin input / tout output
+// blocks: fragment (o/16, i/16) -- o-major (phase.hpp) or, when tout > 0,
+// t-major (phase3.hpp) -- lane (o%16) + 16 ((i/4)%4), component i%4
+__host__ __device__ __forceinline__ long long frag_off(int o, int i, int tin, int tout) {
+  const long long f = tout > 0 ? (long long)(i >> 4) * tout + (o >> 4) : (long long)(o >> 4) * tin + (i >> 4);
+  return ((f * 64 + (o & 15) + 16 * ((i >> 2) & 3)) << 2) + (i & 3);
 }
 
 // --------------------------------------------------------------------------

@@ -52,12 +52,14 @@ def dev():
     return torch.device("cuda:0")
 
 
-def make_solver(pkg, dev, g, fused=True, tnw=True):
+def make_solver(pkg, dev, g, fused=True, tnw=True, phase=None):
     """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at
     create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0)."""
     layers = [int(v) for v in g["layers"]]
     D = layers[0] - 1
     env = {"DBSDE_FUSED": "1" if fused else "0", "DBSDE_TNW": "1" if tnw else "0"}
+    if phase is not None:
+        env["DBSDE_PHASE"] = str(phase)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -229,7 +231,8 @@ def test_net_u_matches_fixture_Y(pkg, dev):
     np.testing.assert_allclose(du.cpu().numpy(), g["Z"].reshape(R, D), rtol=0, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False)], ids=["chain", "splitk_weight_grad"])
+@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False), dict(phase=2)],
+                         ids=["chain", "splitk_weight_grad", "phase2_8wave"])
 def test_kernel_paths_agree_at_north_star(pkg, dev, variant):
     """The default kernels (fused phases + wave-owned weight-gradient tiles)
     against the per-layer chain path and against the split-K weight-gradient
