@@ -63,6 +63,10 @@ struct dbsde_ctx {
   std::string err;
   hipStream_t stream = nullptr;
   int device = 0;
+  // second stream for the short launches that do not feed the next kernel
+  // (weight repack during the rollout, loss sum and grad clear during phase C)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
 
   // ---- network description
   int mode = 0, act = 0, K = 0, D = 0;
@@ -205,6 +209,27 @@ int run(dbsde_ctx* c, const char* name, double flops, double bytes, F&& launch) 
     int rc_ = run(ctx, name, fl, by, [&]() { __VA_ARGS__; }); \
     if (rc_) return rc_;                                   \
   } while (0)
+
+// Queue f() (launches on c->stream) on the side stream, ordered after all
+// work queued so far on the main stream; join_side(i) orders the main stream
+// after it.  Events are recorded on the stream a launch runs on, so the
+// profiler's per-kernel times stay correct.
+template <class F>
+int fork_side(dbsde_ctx* c, int i, F&& f) {
+  HIPC(c, hipEventRecord(c->ev_fork[i], c->stream));
+  HIPC(c, hipStreamWaitEvent(c->side, c->ev_fork[i], 0));
+  hipStream_t main_stream = c->stream;
+  c->stream = c->side;
+  const int rc = f();
+  c->stream = main_stream;
+  if (rc) return rc;
+  HIPC(c, hipEventRecord(c->ev_join[i], c->side));
+  return DBSDE_OK;
+}
+int join_side(dbsde_ctx* c, int i) {
+  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[i], 0));
+  return DBSDE_OK;
+}
 
 // ---------------------------------------------------------------------------
 // fused phase-kernel instantiations: (level tiles T, D tiles TD, blocks K)
@@ -1100,6 +1125,14 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     else if ((e = hipSetDevice(cfg->device)) != hipSuccess) rc = fail(c, DBSDE_EHIP, hipGetErrorString(e));
   }
   if (!rc) rc = build_buffers(c);
+  if (!rc) {
+    hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+      e = hipEventCreateWithFlags(&c->ev_fork[i], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) rc = fail(c, DBSDE_EHIP, std::string("side stream: ") + hipGetErrorString(e));
+  }
   if (rc) {
     g_last_error = c->err;
     dbsde_destroy(c);
@@ -1113,6 +1146,12 @@ void dbsde_destroy(dbsde_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  for (int i = 0; i < 2; ++i) {
+    if (c->ev_fork[i]) (void)hipEventDestroy(c->ev_fork[i]);
+    if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
+  }
+  if (c->side) (void)hipStreamDestroy(c->side);
   for (auto& r : c->pending) {
     c->ev_pool.push_back(r.e0);
     c->ev_pool.push_back(r.e1);
@@ -1150,7 +1189,8 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   const auto& L = c->L;
   const dbsde_problem& pr = c->cfg.problem;
 
-  if ((rc = prep_weights(c, params))) return rc;
+  // weight repack (projection, norms, fragment images) overlaps the rollout
+  if ((rc = fork_side(c, 0, [&]() { return prep_weights(c, params); }))) return rc;
 
   // ---- rollout (network-independent: mu/sigma never read Y, Z)
   if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
@@ -1179,6 +1219,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   }
   const bool q3 = pr.q3 && D == 1;
   if (q3) RUN(c, "q3_sum", 0.0, 4.0 * M * N, q3_sum_kernel<<<N, 256, 0, s>>>(c->sdw, c->Dp, M, N, c->q3S));
+  if ((rc = join_side(c, 0))) return rc;
 
   int nloss_parts;
   FusedArgs fa;
@@ -1251,7 +1292,14 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     nloss_parts = Rp / 256 + 1;
   }
   float* loss_dst = (out && out->loss) ? out->loss : c->loss_tmp;
-  RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, s>>>(c->loss_part, nloss_parts, loss_dst));
+  // loss sum and gradient clear run beside phase C
+  if ((rc = fork_side(c, 1, [&]() {
+         hipStream_t ss = c->stream;
+         RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, ss>>>(c->loss_part, nloss_parts, loss_dst));
+         if (grad) HIPC(c, hipMemsetAsync(grad, 0, (size_t)c->nparams * 4, ss));
+         return DBSDE_OK;
+       })))
+    return rc;
 
   if (grad) {
     if (fv >= 0) {
@@ -1339,8 +1387,8 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
           return rc;
       }
     }
-    // ---- parameter gradients
-    HIPC(c, hipMemsetAsync(grad, 0, (size_t)c->nparams * 4, s));
+    // ---- parameter gradients (grad cleared on the side stream)
+    if ((rc = join_side(c, 1))) return rc;
     if (c->tnw) {
       if ((rc = launch_tnw(c, R, Rp))) return rc;
       if ((rc = finalize_grads(c, params, grad))) return rc;
@@ -1439,6 +1487,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
         export_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, out->X,
                                                                   out->Y, out->Z));
   }
+  if (!grad && (rc = join_side(c, 1))) return rc;
   return DBSDE_OK;
 }
 

@@ -59,6 +59,11 @@ struct Mat {
 // second derivative (one sincosf / tanhf per element)
 template <int ACT>
 __device__ __forceinline__ void act_v1(float a, float& f, float& d1) {
+#ifdef DBSDE_EXP_CHEAPACT
+  f = a;   // timing experiment only: no transcendental epilogue
+  d1 = 1.f;
+  return;
+#endif
   if constexpr (ACT == ACT_SINE) {
     fast_sincosf(a, f, d1);
   } else if constexpr (ACT == ACT_TANH) {
@@ -71,6 +76,9 @@ __device__ __forceinline__ void act_v1(float a, float& f, float& d1) {
 }
 template <int ACT>
 __device__ __forceinline__ float act_1(float a) {
+#ifdef DBSDE_EXP_CHEAPACT
+  return a;
+#endif
   if constexpr (ACT == ACT_SINE) {
     float sv, cv;
     fast_sincosf(a, sv, cv);
@@ -84,6 +92,11 @@ __device__ __forceinline__ float act_1(float a) {
 }
 template <int ACT>
 __device__ __forceinline__ void act_12(float a, float& d1, float& d2) {
+#ifdef DBSDE_EXP_CHEAPACT
+  d1 = a;
+  d2 = 1.f;
+  return;
+#endif
   if constexpr (ACT == ACT_SINE) {
     float sv;
     fast_sincosf(a, sv, d1);

@@ -20,12 +20,27 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 enum Act { ACT_SINE = 0, ACT_RELU = 1, ACT_TANH = 2 };
 
-// sin and cos together: Cody-Waite reduction with a 3-part pi/2 in fp32 for
-// |a| <= 8192 (fp64 reduction above), cephes minimax polynomials in fp32 on
-// [-pi/4, pi/4].  Max abs error < 0.8 * 2^-23 for |a| <= 2e4 (host-tested
-// against libm in fp64).  Far fewer registers and VALU cycles than the library
-// sincosf, whose large-argument path is allocated for every unrolled element.
+// sin and cos together on the transcendental unit: a is reduced modulo 2*pi in
+// radians (two-part Cody-Waite 2*pi in fp32, |r| <= pi), scaled to revolutions
+// and fed to v_sin_f32 / v_cos_f32 (sin(2*pi*x), quarter rate).  7 VALU-slot
+// equivalents per element instead of ~25 for the polynomial below; the phase
+// kernels evaluate it 4 (phase A) and 8 (phase C) times per activation element.
+// Max abs error ~3e-7 (2.5 ulp of 1), independent of |a| because the
+// reduction happens before the scaling (tools/ubench/sincos_acc.hip measures
+// it against fp64 libm on the GPU; the plain fract-of-a/(2pi) form grows to
+// 5.5e-6 at |a| = 64).  DBSDE_SINCOS_POLY selects the polynomial (A/B only).
 __device__ __forceinline__ void fast_sincosf(float a, float& s, float& c) {
+#ifndef DBSDE_SINCOS_POLY
+  const float k = rintf(a * 0.15915494309189535f);
+  float r = fmaf(-k, 6.2831854820251465f, a);   // 2pi_hi = fp32(2pi)
+  r = fmaf(-k, -1.7484555314695172e-07f, r);    // 2pi_lo = 2pi - 2pi_hi
+  const float rev = r * 0.15915494309189535f;   // [-1/2, 1/2]
+  s = __builtin_amdgcn_sinf(rev);
+  c = __builtin_amdgcn_cosf(rev);
+#else
+  // Cody-Waite reduction with a 3-part pi/2 in fp32 for |a| <= 8192 (fp64
+  // reduction above), cephes minimax polynomials in fp32 on [-pi/4, pi/4];
+  // max abs error < 0.8 * 2^-23 for |a| <= 2e4.
   float r;
   int m;
   if (__builtin_expect(fabsf(a) <= 8192.f, 1)) {
@@ -45,6 +60,7 @@ __device__ __forceinline__ void fast_sincosf(float a, float& s, float& c) {
       1.0f - 0.5f * z + z * z * (4.166664568298827e-2f + z * (-1.388731625493765e-3f + z * 2.443315711809948e-5f));
   s = (m == 0) ? sp : (m == 1) ? cp : (m == 2) ? -sp : -cp;
   c = (m == 0) ? cp : (m == 1) ? -sp : (m == 2) ? -cp : sp;
+#endif
 }
 __device__ __forceinline__ float act_f(int act, float a) {
   if (act == ACT_SINE) {

@@ -41,6 +41,9 @@ __device__ __forceinline__ void bload(Mat<TT>& m, const float* base, int ld, int
 }
 template <int TT>
 __device__ __forceinline__ void bstore(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
+#ifdef DBSDE_EXP_NOSTORE
+  if (base != nullptr) return;   // timing experiment only: activation stores dropped
+#endif
   const int lane = threadIdx.x & 63;
   float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);
 #pragma unroll

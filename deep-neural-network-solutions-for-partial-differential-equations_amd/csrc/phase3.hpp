@@ -59,6 +59,12 @@ struct PieceStager {
   const int* nf;
   int n, st, wave, lane, buf;
   __device__ __forceinline__ const floatx4* next() {
+#ifdef DBSDE_EXP_NOSTAGE
+    if (st++ > 0) return wl;   // timing experiment only: every piece reuses piece 0, no DMA, no barrier
+    vm_wait0();
+    __syncthreads();
+    return wl;
+#endif
     vm_wait0();
     __syncthreads();
     if (st + 1 < n) piece_dma(img[st + 1], nf[st + 1], wl + ((st + 1) & 1) * buf, wave, lane);
