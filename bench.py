@@ -6,10 +6,13 @@ One step = one optimizer iteration over one synthetic minibatch: Brownian
 increments drawn on the device (Philox), Euler-Maruyama rollout, network
 forward + Z, residual loss, second-order backward, [RCCL all-reduce], Adam.
 All inputs resident in HBM.  value = total SDE path-steps/s over all ranks
-(weak scaling: 1024 paths per GPU).
+(weak scaling: 1024 paths per GPU; --strong: 1024 paths in total, split).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+--workload basket|hjb|heston runs BASELINE configs 3-5 on this process's GPUs
+(separate lines for DESIGN.md; the headline is the default bsb workload).
 """
 from __future__ import annotations
 
@@ -36,16 +39,34 @@ LR = 1e-3
 U0_EXACT = float(np.exp((0.05 + 0.4 ** 2) * 1.0) * 62.5)     # DeepBSDE.py:345-349 at Xi=[1,.5]*50
 PEAK_FP32_MFMA_TFLOPS = 157.3                                # MI355X_MICROARCH.md, dense f32 MFMA
 PEAK_HBM_GBS = 8000.0
-# rocprof symbol suffix of the phase kernels the library launches (DBSDE_PHASE, default 3)
-PHASE_SUFFIX = {"1": "", "2": "2"}.get(os.environ.get("DBSDE_PHASE", "3"), "3")
+PROFILE_ROUND = "r2"          # profiles/<round>_pmc_* counter collections of the current build
 # rocprof symbol of each profiled launch class (EPI ids from csrc/kernels.hpp)
 KERNEL_SYMBOL = {
     "gemm_xstack_fwd": "chain_gemm_kernel<7, 0>", "gemm_block_fwd": "chain_gemm_kernel<7, 1>",
     "gemm_block_inputgrad": "chain_gemm_kernel<7, 2>", "gemm_z_cotangent": "chain_gemm_kernel<7, 3>",
     "gemm_xstack_tangent": "chain_gemm_kernel<7, 4>", "gemm_block_tangent": "chain_gemm_kernel<7, 5>",
     "gemm_block_reverse": "chain_gemm_kernel<7, 6>", "tn_weight_grad": "tnw_kernel",
-    "fused_fwd_inputgrad": f"phaseA{PHASE_SUFFIX}_kernel", "fused_tangent_reverse": f"phaseC{PHASE_SUFFIX}_kernel",
-    "rollout": "rollout_kernel", "cotangent": "cotan_kernel", "grad_finalize": "slabsum_kernel",
+    "fused_fwd_inputgrad": "phaseA_kernel", "fused_tangent_reverse": "phaseC_kernel",
+    "rollout": "rollout_kernel", "grad_finalize": "slabsum_kernel",
+}
+MFMA_LAUNCHES = ("fused_fwd_inputgrad", "fused_tangent_reverse", "tn_weight_grad", "gemm_")
+
+# BASELINE.json configs (the headline is "bsb")
+WORKLOADS = {
+    "bsb": dict(cls="BlackScholesBarenblatt", D=100, layers=[101] + 4 * [110] + [1], mode="NAIS-Net",
+                act="Sine", M=1024, N=50, xi="bsb",
+                desc="100-D Black-Scholes-Barenblatt deep-BSDE training step (DeepBSDE.py semantics: Adam lr "
+                     "1e-3, no clip)"),
+    "basket": dict(cls="BasketCallOption", D=100, layers=[101] + 4 * [110] + [1], mode="Naisnet", act="ReLU",
+                   M=4096, N=50, xi="ones",
+                   desc="100-D basket call, Cholesky-correlated device increments (Q10 matrix), Naisnet-ReLU "
+                        "(with_corr_high_dimension_pde.py semantics: Adam, clip 1.0)"),
+    "hjb": dict(cls="HamiltonJacobiBellman", D=100, layers=[101] + 4 * [256] + [1], mode="FC", act="Sine",
+                M=2048, N=20, xi="zeros", desc="100-D HJB, FC-Sine [101,256x4,1] (hjb_implement.py semantics)"),
+    "heston": dict(cls="HestonFBSNN", D=50, layers=[51] + 4 * [110] + [1], mode="Naisnet", act="Sine",
+                   M=1024, N=100, xi="ones",
+                   desc="50-asset Heston (state 100), Naisnet-Sine (heston_dnnpde.py semantics generalised to "
+                        "k assets: clamps, u >= 0, NaN skip, clip 1.0)"),
 }
 
 
@@ -53,10 +74,11 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(seconds):
+def cpu_baseline(iters=10, warmup=2):
     """The oracle's faithful torch-CPU restatement of the reference step
     (fetch_minibatch + loss_function + double backward + Adam, anomaly mode
-    off), timed on the host cores on a bounded sample of iterations."""
+    off), timed on the host cores: `warmup` untimed iterations, then `iters`
+    timed ones; median and spread reported."""
     from oracle import fbsnn_ref as fr
     torch.manual_seed(0)
     np.random.seed(0)
@@ -64,19 +86,19 @@ def cpu_baseline(seconds):
     prob = fr.make_problem("bsb", D)
     Xi = np.array([1.0, 0.5] * (D // 2))[None, :]
     times = []
-    t_start = time.time()
-    while time.time() - t_start < seconds or len(times) < 2:
+    for i in range(warmup + iters):
         t0 = time.time()
         fr.train(model, prob, Xi, M_PER_GPU, N_STEPS, D, T, 1, LR, clip=False)
-        times.append(time.time() - t0)
-        if len(times) >= 50:
-            break
-    per_iter = float(np.median(times[1:])) if len(times) > 2 else float(np.mean(times))
-    return {"value": M_PER_GPU * N_STEPS / per_iter, "unit": "path-steps/s", "cores": torch.get_num_threads(),
+        if i >= warmup:
+            times.append(time.time() - t0)
+    med = float(np.median(times))
+    return {"value": M_PER_GPU * N_STEPS / med, "unit": "path-steps/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"{len(times)} full training iterations of the same workload (M=1024, N=50, D=100, "
-                      f"NAIS-Net 4x110 Sine, Adam) by oracle/fbsnn_ref.py (torch CPU, autograd double "
-                      f"backward, dense diag sigma, anomaly off), median {per_iter:.3f} s/iteration"}
+            "sample": f"{iters} timed training iterations after {warmup} warm-up of the same workload (M=1024, "
+                      f"N=50, D=100, NAIS-Net 4x110 Sine, Adam) by oracle/fbsnn_ref.py (torch CPU, autograd "
+                      f"double backward, dense diag sigma, anomaly off): median {med:.3f} s/iteration, "
+                      f"min {min(times):.3f}, max {max(times):.3f}",
+            "s_per_iter": {"median": med, "min": float(min(times)), "max": float(max(times))}}
 
 
 def traffic_from_pmc(symbol, launches_per_step):
@@ -84,7 +106,7 @@ def traffic_from_pmc(symbol, launches_per_step):
     counter collection (profiles/*pmc*counter_collection.csv): FETCH_SIZE is
     doubled (gfx950 reports half of wide coalesced reads, MI355X_MICROARCH.md
     HBM section), WRITE_SIZE taken as is; both counters are in KB."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*counter_collection.csv")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc*counter_collection.csv")))
     if not files:
         return None
     sums = {"FETCH_SIZE": [], "WRITE_SIZE": []}
@@ -98,15 +120,40 @@ def traffic_from_pmc(symbol, launches_per_step):
     return 1024.0 * (2.0 * np.mean(sums["FETCH_SIZE"]) + np.mean(sums["WRITE_SIZE"]))
 
 
+def build_model(pkg, wl, M, dev, args):
+    cls = getattr(pkg, wl["cls"])
+    Dw = wl["D"]
+    if wl["xi"] == "bsb":
+        Xi = np.array([1.0, 0.5] * (Dw // 2))[None, :]
+    elif wl["xi"] == "zeros":
+        Xi = np.zeros((1, Dw))
+    else:
+        Xi = np.ones((1, Dw))
+    mode = args.mode or wl["mode"]
+    act = args.activation or wl["act"]
+    if wl["cls"] == "BlackScholesBarenblatt":
+        return cls(Xi, T, M, wl["N"], Dw, wl["layers"], mode, act, device=dev), Xi
+    if wl["cls"] == "HamiltonJacobiBellman":
+        return cls(Xi, T, M, wl["N"], Dw, wl["layers"], mode, act, device=dev), Xi
+    if wl["cls"] == "BasketCallOption":
+        np.random.seed(0)                      # the Q10 correlation matrix draw
+        m = cls(Xi, T, M, wl["N"], Dw, None, wl["layers"], mode, act, "random_correlation", device=dev)
+        m.N = wl["N"]
+        return m, Xi
+    return cls(Xi, T, M, wl["N"], Dw, None, wl["layers"], mode, act, device=dev), Xi
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)      # >= 50 steps after >= 10 warm-up
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--strong", action="store_true", help="global batch fixed at the workload's M (split)")
+    ap.add_argument("--workload", default="bsb", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--activation", default="Sine", help="experiments only; the headline is Sine")
-    ap.add_argument("--mode", default="NAIS-Net", help="experiments only; the headline is NAIS-Net")
+    ap.add_argument("--activation", default=None, help="experiments only; the headline is Sine")
+    ap.add_argument("--mode", default=None, help="experiments only; the headline is NAIS-Net")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -119,12 +166,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    wl = WORKLOADS[args.workload]
     pkg = importlib.import_module(PKG)
     torch.manual_seed(0)
-    Xi = np.array([1.0, 0.5] * (D // 2))[None, :]
-    model = pkg.BlackScholesBarenblatt(Xi, T, M_PER_GPU * world, N_STEPS, D, LAYERS, args.mode, args.activation,
-                                       device=dev)
-    opt = model.new_optimizer_state()
+    M_global = wl["M"] if args.strong else wl["M"] * world
+    model, Xi = build_model(pkg, wl, M_global, dev, args)
+    opt = model.new_optimizer_state("Adam", LR)
 
     def barrier():
         if world > 1:
@@ -148,6 +195,19 @@ def main():
         elapsed = float(e)
     final_loss = float(loss)
 
+    # the one collective per step, alone: [grad | loss] all-reduce latency
+    allreduce_us = None
+    if world > 1:
+        buf = model._gradbuf.clone()
+        for _ in range(5):
+            dist.all_reduce(buf)
+        barrier()
+        ta = time.perf_counter()
+        for _ in range(20):
+            dist.all_reduce(buf)
+        barrier()
+        allreduce_us = 1e6 * (time.perf_counter() - ta) / 20
+
     # per-kernel HIP-event timing of the same K steps (separate window so the
     # headline time carries no event overhead)
     model.solver.profile(True)
@@ -158,7 +218,7 @@ def main():
     prof = model.solver.profile_read()
     model.solver.profile(False)
 
-    u0, _ = model.net_u(torch.zeros(1), torch.from_numpy(Xi).float())
+    u0, _ = model.net_u(torch.zeros(1), model.Xi.reshape(1, -1))
     u0 = float(u0)
 
     if rank != 0:
@@ -167,28 +227,39 @@ def main():
         return
 
     ms_per_step = 1000.0 * elapsed / args.steps
-    total_path_steps = M_PER_GPU * world * N_STEPS
+    total_path_steps = M_global * wl["N"]
     value = total_path_steps * args.steps / elapsed
 
-    dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
-    name, st = dom
+    # roofline of the dominant MFMA kernel (the main-stream network passes;
+    # side-stream launches such as loss_final include queue wait in their events)
+    mfma = {k: v for k, v in prof.items() if k.startswith(MFMA_LAUNCHES)}
+    name, st = max(mfma.items(), key=lambda kv: kv[1]["ms"])
     avg_ms = st["ms"] / st["launches"]
-    is_mfma = name.startswith(("gemm", "tn_", "fused_"))
-    if is_mfma:
-        achieved = st["flops"] / st["launches"] / (avg_ms * 1e-3) / 1e12
-        peak, unit = PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
-    else:
-        achieved = st["bytes"] / st["launches"] / (avg_ms * 1e-3) / 1e9
-        peak, unit = PEAK_HBM_GBS, "GB/s"
+    achieved = st["flops"] / st["launches"] / (avg_ms * 1e-3) / 1e12
     symbol = KERNEL_SYMBOL.get(name, name)
-    traffic = traffic_from_pmc(symbol, st["launches"] / args.steps)
+    traffic = traffic_from_pmc(symbol, st["launches"] / args.steps) if args.workload == "bsb" else None
+    roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic, "kernel": f"{name} ({symbol})",
+                "avg_launch_ms": avg_ms, "launches_per_step": st["launches"] / args.steps,
+                "alg_flops_per_launch": st["flops"] / st["launches"]}
+    # the path-step kernel against HBM (north_star: achieved GB/s of the path step)
+    rp = prof.get("rollout")
+    roofline_path = None
+    if rp:
+        r_ms = rp["ms"] / rp["launches"]
+        gbs = rp["bytes"] / rp["launches"] / (r_ms * 1e-3) / 1e9
+        roofline_path = {"bound": "hbm", "achieved": gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": gbs / PEAK_HBM_GBS, "kernel": "rollout", "avg_launch_ms": r_ms,
+                         "alg_bytes_per_launch": rp["bytes"] / rp["launches"],
+                         "traffic": traffic_from_pmc("rollout", 1.0) if args.workload == "bsb" else None}
     step_flops = sum(v["flops"] for v in prof.values()) / args.steps
     breakdown = {k: round(v["ms"] / args.steps, 4) for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
 
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+    if world == 1 and not args.no_cpu_baseline and args.workload == "bsb":
+        cpu = cpu_baseline(args.cpu_iters)
 
+    Mloc = M_global // world
     out = {
         "metric": "SDE-path-steps/sec + |u(0,X_0) err|, 100-D BSB, 1/2/4/8 MI355X",
         "value": value,
@@ -198,23 +269,23 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: device Philox Brownian increments, reference (xavier) init weights, seed 0",
-        "config": {"workload": "100-D Black-Scholes-Barenblatt deep-BSDE training step "
-                               "(DeepBSDE.py semantics: Adam lr 1e-3, no clip)",
-                   "D": D, "layers": LAYERS, "mode": args.mode, "activation": args.activation,
-                   "paths_per_gpu": M_PER_GPU, "global_batch": M_PER_GPU * world, "time_steps": N_STEPS,
+        "config": {"workload": wl["desc"], "name": args.workload, "D": wl["D"], "layers": wl["layers"],
+                   "mode": args.mode or wl["mode"], "activation": args.activation or wl["act"],
+                   "paths_per_gpu": Mloc, "global_batch": M_global, "time_steps": wl["N"],
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma" if is_mfma else "hbm", "achieved": achieved, "peak": peak, "unit": unit,
-                     "frac": achieved / peak, "traffic": traffic, "kernel": f"{name} ({symbol})",
-                     "avg_launch_ms": avg_ms, "launches_per_step": st["launches"] / args.steps,
-                     "alg_flops_per_launch": st["flops"] / st["launches"]},
+        "roofline": roofline,
+        "roofline_path_step": roofline_path,
+        "allreduce_us": allreduce_us,
+        "per_gpu_path_steps_per_s": value / world,
         "step_alg_tflops": step_flops / (ms_per_step * 1e-3) / 1e12,
         "step_kernel_ms": breakdown,
-        "accuracy": {"u0": u0, "u0_exact": U0_EXACT, "abs_err": abs(u0 - U0_EXACT), "train_iterations": it,
-                     "final_loss": final_loss,
+        "accuracy": {"u0": u0, "u0_exact": U0_EXACT if args.workload == "bsb" else None,
+                     "abs_err": abs(u0 - U0_EXACT) if args.workload == "bsb" else None,
+                     "train_iterations": it, "final_loss": final_loss,
                      "note": "parity |u0 - reference| < 1e-3 is tested in tests/test_gpu_parity.py; the exact "
                              "value needs ~2e4 iterations of training"},
         "cpu_baseline": cpu,

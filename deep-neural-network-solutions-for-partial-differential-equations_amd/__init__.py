@@ -12,9 +12,10 @@ Import it with importlib (the directory name is not a Python identifier):
 """
 from . import _lib
 from .deepbsde import BlackScholesBarenblatt, u_exact
-from .fbsnn import FBSNN
-from .problems import BasketCallOption, BSPDETestCase, CallOption, CallOption1D, HamiltonJacobiBellman
-from .solver import NativeSolver, ProblemSpec
+from .fbsnn import FBSNN, PredictionGenerator
+from .problems import BasketCallOption, BSPDETestCase, CallOption, CallOption1D, HamiltonJacobiBellman, HestonFBSNN
+from .solver import NativeSolver, ProblemSpec, exact, hjb_mc
 
-__all__ = ["FBSNN", "BlackScholesBarenblatt", "u_exact", "CallOption", "CallOption1D", "BasketCallOption",
-           "BSPDETestCase", "HamiltonJacobiBellman", "NativeSolver", "ProblemSpec", "_lib"]
+__all__ = ["FBSNN", "PredictionGenerator", "BlackScholesBarenblatt", "u_exact", "CallOption", "CallOption1D",
+           "BasketCallOption", "BSPDETestCase", "HamiltonJacobiBellman", "HestonFBSNN", "NativeSolver",
+           "ProblemSpec", "exact", "hjb_mc", "_lib"]

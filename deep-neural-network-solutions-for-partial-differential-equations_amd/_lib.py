@@ -16,22 +16,28 @@ DBSDE_OK, DBSDE_EINVAL, DBSDE_EHIP, DBSDE_ENOMEM = 0, -1, -2, -3
 
 MODES = {"FC": 0, "NAIS-Net": 1, "Resnet": 2, "Naisnet": 3}
 ACTIVATIONS = {"Sine": 0, "ReLU": 1, "Tanh": 2}
-G_KINDS = {"sumsq": 0, "call_sum": 1, "call_mean": 2, "log": 3}
-OPTIMIZERS = {"Adam": 0, "AdamW": 1, "SGD": 2}
+G_KINDS = {"sumsq": 0, "call_sum": 1, "call_mean": 2, "log": 3, "smooth_call": 4}
+PROBLEM_KINDS = {"diag": 0, "heston": 1}
+OPTIMIZERS = {"Adam": 0, "AdamW": 1, "SGD": 2, "RMSprop": 3, "Adagrad": 4, "Adamax": 5, "Adadelta": 6, "ASGD": 7}
+EXACT_KINDS = {"bsb": 0, "bs_call": 1, "basket_avg": 2, "basket_mean": 3}
+ABI_VERSION = 2
 
 # every symbol include/dbsde.h declares (checked by the CPU test suite)
 EXPORTED = [
     "dbsde_abi_version", "dbsde_create", "dbsde_destroy", "dbsde_last_error", "dbsde_set_stream",
-    "dbsde_param_count", "dbsde_param_used_mask", "dbsde_loss_grad", "dbsde_net_u",
-    "dbsde_optimizer_step", "dbsde_profile_enable", "dbsde_profile_count", "dbsde_profile_read",
-    "dbsde_profile_reset",
+    "dbsde_param_count", "dbsde_param_used_mask", "dbsde_brownian_dim", "dbsde_set_corr", "dbsde_brownian",
+    "dbsde_loss_grad", "dbsde_net_u", "dbsde_optimizer_step", "dbsde_exact", "dbsde_hjb_mc",
+    "dbsde_profile_enable", "dbsde_profile_count", "dbsde_profile_read", "dbsde_profile_reset",
 ]
 
 
 class Problem(ctypes.Structure):
-    _fields_ = [("mu_a", ctypes.c_float), ("sig_a", ctypes.c_float), ("sig_b", ctypes.c_float),
-                ("phi_r", ctypes.c_float), ("phi_c", ctypes.c_float), ("phi_zz", ctypes.c_float),
-                ("g_kind", ctypes.c_int), ("strike", ctypes.c_float), ("q3", ctypes.c_int)]
+    _fields_ = [("kind", ctypes.c_int), ("mu_a", ctypes.c_float), ("sig_a", ctypes.c_float),
+                ("sig_b", ctypes.c_float), ("phi_r", ctypes.c_float), ("phi_c", ctypes.c_float),
+                ("phi_zz", ctypes.c_float), ("g_kind", ctypes.c_int), ("strike", ctypes.c_float),
+                ("q3", ctypes.c_int), ("g_cols", ctypes.c_int), ("g_alpha", ctypes.c_float),
+                ("u_clamp", ctypes.c_int), ("h_kappa", ctypes.c_float), ("h_theta", ctypes.c_float),
+                ("h_sigma", ctypes.c_float), ("h_rho", ctypes.c_float)]
 
 
 class Config(ctypes.Structure):
@@ -55,7 +61,9 @@ class Outputs(ctypes.Structure):
 class Optim(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int), ("lr", ctypes.c_float), ("beta1", ctypes.c_float),
                 ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
-                ("max_norm", ctypes.c_float), ("step", ctypes.c_longlong)]
+                ("max_norm", ctypes.c_float), ("step", ctypes.c_longlong), ("alpha", ctypes.c_float),
+                ("rho", ctypes.c_float), ("lr_decay", ctypes.c_float), ("lambd", ctypes.c_float),
+                ("asgd_eta", ctypes.c_float), ("asgd_mu", ctypes.c_float), ("loss", ctypes.c_void_p)]
 
 
 _LIB = None
@@ -79,6 +87,11 @@ def load():
         "dbsde_set_stream": (i, [vp, vp]),
         "dbsde_param_count": (ll, [vp]),
         "dbsde_param_used_mask": (i, [vp, vp, ll]),
+        "dbsde_brownian_dim": (i, [vp]),
+        "dbsde_set_corr": (i, [vp, vp, i]),
+        "dbsde_brownian": (i, [vp, ctypes.POINTER(Batch), vp, vp, i]),
+        "dbsde_exact": (i, [i, vp, vp, ll, i, ctypes.c_float, vp, vp, vp, vp]),
+        "dbsde_hjb_mc": (i, [vp, vp, i, i, ctypes.c_float, ll, ctypes.c_ulonglong, vp, vp]),
         "dbsde_loss_grad": (i, [vp, vp, ctypes.POINTER(Batch), vp, ctypes.POINTER(Outputs)]),
         "dbsde_net_u": (i, [vp, vp, i, vp, vp, vp, vp]),
         "dbsde_optimizer_step": (i, [vp, vp, vp, vp, vp, ctypes.POINTER(Optim)]),
@@ -93,7 +106,7 @@ def load():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.dbsde_abi_version() != 1:
+    if lib.dbsde_abi_version() != ABI_VERSION:
         raise RuntimeError("libdbsde ABI version mismatch")
     _LIB = lib
     return lib

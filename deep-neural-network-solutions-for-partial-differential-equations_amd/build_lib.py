@@ -11,7 +11,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 # translation units and their extra flags: the weight-gradient kernel is built
 # with VGPR-form MFMA (see csrc/tnw.hip); everything else with the defaults
-UNITS = [("engine.hip", []), ("tnw.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=true"])]
+UNITS = [("engine.hip", []), ("evals.hip", []), ("tnw.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=true"])]
 DEPS = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith((".hip", ".hpp"))] + \
     [os.path.join(ROOT, "include", "dbsde.h")]
 OUT = os.path.join(HERE, "lib", "libdbsde.so")

@@ -23,9 +23,8 @@
 
 #include "../../include/dbsde.h"
 #include "kernels.hpp"
-#include "fused.hpp"
+#include "paths.hpp"
 #include "phase.hpp"
-#include "phase3.hpp"
 #include "tnw.hpp"
 
 using namespace dbsde;
@@ -67,9 +66,14 @@ struct dbsde_ctx {
   // (weight repack during the rollout, loss sum and grad clear during phase C)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
+  bool side_pending[2] = {false, false};
 
   // ---- network description
   int mode = 0, act = 0, K = 0, D = 0;
+  int nb = 0;                 // Brownian dimension (D; D/2 for Heston)
+  int gcols = 0;              // state columns entering g and the terminal Z loss
+  bool heston = false, u_clamp = false;
+  float* Lt = nullptr;        // correlated device mode: L^T [nb][nb] (dbsde_set_corr)
   std::vector<int> L;
   bool has_v = false, proj = false;
   float rho = 0.f;
@@ -107,7 +111,7 @@ struct dbsde_ctx {
   float *Abuf = nullptr, *Adot = nullptr, *Delta = nullptr, *Alpha = nullptr, *H = nullptr, *Hdot = nullptr,
         *G = nullptr;
   float* Pbuf[2] = {nullptr, nullptr};
-  float *u = nullptr, *rres = nullptr, *lossrow = nullptr, *ubar = nullptr, *q3S = nullptr;
+  float *u = nullptr, *rres = nullptr, *lossrow = nullptr, *ubar = nullptr, *q3S = nullptr, *umask = nullptr;
   float *u16 = nullptr, *o16 = nullptr;  // [Rp,16]: col 0 = ubar / 1 (output-layer TN operands)
   double* loss_part = nullptr;
   float* loss_tmp = nullptr;
@@ -117,7 +121,6 @@ struct dbsde_ctx {
 
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
-  int phase_ver = 3;              // DBSDE_PHASE=1|2|3: fused.hpp (LDS relayout) / phase.hpp (8-wave) / phase3.hpp (4-wave)
   // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
   // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
   std::vector<float*> imgX, imgZ, imgF, imgB;
@@ -237,14 +240,8 @@ struct FusedVariant {
   int T, TD, K, act;
   void (*A)(FusedArgs);
   void (*C)(FusedArgs);
-  void (*A2)(FusedArgs);
-  void (*C2)(FusedArgs);
-  void (*A3)(FusedArgs);
-  void (*C3)(FusedArgs);
 };
-#define FV(T, TD, K, ACT)                                                                            \
-  {T, TD, K, ACT, phaseA_kernel<T, TD, K, ACT>, phaseC_kernel<T, TD, K, ACT>, phaseA2_kernel<T, TD, K, ACT>, \
-   phaseC2_kernel<T, TD, K, ACT>, phaseA3_kernel<T, TD, K, ACT>, phaseC3_kernel<T, TD, K, ACT>}
+#define FV(T, TD, K, ACT) {T, TD, K, ACT, phaseA_kernel<T, TD, K, ACT>, phaseC_kernel<T, TD, K, ACT>}
 const FusedVariant kFused[] = {
     FV(7, 7, 3, 0), FV(7, 7, 3, 1), FV(7, 7, 3, 2), FV(1, 1, 1, 0), FV(1, 1, 1, 1), FV(1, 1, 1, 2),
     FV(1, 1, 2, 0), FV(1, 1, 2, 1), FV(1, 1, 2, 2), FV(1, 1, 3, 0), FV(1, 1, 3, 1), FV(1, 1, 3, 2),
@@ -351,8 +348,17 @@ int build_net(dbsde_ctx* c) {
   const char* env = getenv("DBSDE_FUSED");
   const bool allow = !(env && env[0] == '0');
   c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act) >= 0;
-  const char* pv = getenv("DBSDE_PHASE");
-  c->phase_ver = pv ? std::max(1, std::min(3, atoi(pv))) : 3;
+  // problem kind: Brownian dimension, g columns, u clamp
+  const dbsde_problem& pr = g.problem;
+  if (pr.kind != DBSDE_PROB_DIAG && pr.kind != DBSDE_PROB_HESTON) return fail(c, DBSDE_EINVAL, "unknown problem kind");
+  if (pr.g_kind < 0 || pr.g_kind > 4) return fail(c, DBSDE_EINVAL, "unknown terminal condition");
+  c->heston = pr.kind == DBSDE_PROB_HESTON;
+  if (c->heston && c->D % 2 != 0)
+    return fail(c, DBSDE_EINVAL, "Heston state is [S_1..S_k, v_1..v_k]: layers[0] - 1 must be even");
+  c->nb = c->heston ? c->D / 2 : c->D;
+  c->gcols = pr.g_cols > 0 ? pr.g_cols : c->D;
+  if (c->gcols > c->D) return fail(c, DBSDE_EINVAL, "g_cols exceeds the state dimension");
+  c->u_clamp = pr.u_clamp != 0;
   return DBSDE_OK;
 }
 
@@ -442,11 +448,10 @@ int build_buffers(dbsde_ctx* c) {
       if ((rc = dalloc_t(c, &c->imgB[j], (size_t)TW * TW * 256))) return rc;
     }
   }
-  const bool tmajor = c->phase_ver == 3;
-  auto frag = [tmajor](PackDesc d, float* img, int tin, int tout, int row0, int col0) {
+  auto frag = [](PackDesc d, float* img, int tin, int tout, int row0, int col0) {
     d.fdst = img;
     d.ftin = tin;
-    d.ftout = tmajor ? tout : 0;
+    d.ftout = tout;
     d.frow0 = row0;
     d.fcol0 = col0;
     return d;
@@ -577,6 +582,15 @@ int build_buffers(dbsde_ctx* c) {
     slabsum(K + 1, 0, 0, 1, c->out.in, gtag(c->out.w), 1, 1.f);
     slabsum(K + 1, 0, c->Wp[K], 1, 1, gtag(c->out.b), 1, 1.f);
   }
+  if (c->mode == DBSDE_MODE_NAIS_NET) {
+    // Q6: input_layers[K] never receives a gradient; its slots are written as
+    // zeros here so the gradient buffer needs no clearing memset
+    const long long tail = (long long)c->L[c->cfg.n_layers - 2] * c->L[0] + c->L[c->cfg.n_layers - 2];
+    PackDesc d = mk_desc(gtag(c->nparams - tail), 1, gtag(c->nparams - tail), (int)tail, 1, (int)tail, 0,
+                         PK_SLABSUM, 1.f);
+    d.nslab = 0;
+    F.push_back(d);
+  }
   c->n_fin = (int)F.size();
   c->fin_blocks = 1;
   for (const PackDesc& d : F) c->fin_blocks = std::max(c->fin_blocks, (d.rows * d.cols + 63) / 64);
@@ -621,6 +635,7 @@ int ensure_rows(dbsde_ctx* c, int Rp, int N) {
   if ((rc = dalloc_t(c, &c->rres, R))) return rc;
   if ((rc = dalloc_t(c, &c->lossrow, R))) return rc;
   if ((rc = dalloc_t(c, &c->ubar, R))) return rc;
+  if ((rc = dalloc_t(c, &c->umask, R))) return rc;
   if ((rc = dalloc_t(c, &c->u16, R * 16))) return rc;
   if ((rc = dalloc_t(c, &c->o16, R * 16))) return rc;
   fill_col0_kernel<<<(unsigned)((R + 255) / 256), 256, 0, c->stream>>>(c->o16, 16, (long long)R, 1.f);
@@ -670,6 +685,59 @@ ChainArgs base_args(dbsde_ctx* c) {
   a.rho = c->rho;
   a.act = c->act;
   return a;
+}
+
+constexpr int ROW_PAD = 64;   // rows per phase-kernel workgroup (P3_ROWS) and chain-GEMM tile
+
+RolloutArgs rollout_args(dbsde_ctx* c, const dbsde_batch* b) {
+  const dbsde_problem& pr = c->cfg.problem;
+  RolloutArgs ra{};
+  ra.M = b->M;
+  ra.N = b->N;
+  ra.D = c->D;
+  ra.ldx = c->Dp;
+  ra.nb = c->nb;
+  ra.t = b->t;
+  ra.W = b->W;
+  ra.Xi = b->Xi;
+  ra.xi_rows = b->xi_rows;
+  ra.T = c->cfg.T;
+  ra.seed = b->seed;
+  ra.offset = b->offset;
+  ra.path0 = b->path0;
+  ra.mu_a = pr.mu_a;
+  ra.sig_a = pr.sig_a;
+  ra.sig_b = pr.sig_b;
+  ra.kappa = pr.h_kappa;
+  ra.theta = pr.h_theta;
+  ra.hsig = pr.h_sigma;
+  ra.rho = pr.h_rho;
+  ra.Lt = c->Lt;
+  ra.xin = c->xin;
+  ra.sdw = c->sdw;
+  return ra;
+}
+
+// Euler-Maruyama paths (ra.out == PATH_ROLLOUT) or the device fetch_minibatch
+// (PATH_FETCH_*): Heston, Cholesky-correlated device mode, or diagonal
+int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
+  hipStream_t s = c->stream;
+  const char* name = ra.out == PATH_ROLLOUT ? "rollout" : "brownian";
+  const double steps = (double)ra.M * ra.N;
+  const double bytes = ra.out == PATH_ROLLOUT ? 4.0 * steps * (2.0 * ra.D + (ra.W ? ra.nb : 0)) : 4.0 * steps * ra.nb;
+  if (c->heston) {
+    const int nthr = ra.M * ra.nb;
+    RUN(c, name, 0.0, bytes, rollout_heston_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
+  } else if (c->Lt && !ra.W) {
+    const int G = (ra.nb + 63) / 64 * 64, PB = (256 / G) * CP_PPT;
+    const size_t smem = ((size_t)((ra.nb * ra.nb + 3) & ~3) + 2 * (size_t)ra.nb * PB) * sizeof(float);
+    RUN(c, name, 2.0 * steps * ra.nb * ra.nb / 2, bytes,
+        rollout_corr_kernel<<<(ra.M + PB - 1) / PB, 256, smem, s>>>(ra));
+  } else {
+    const int nthr = ra.M * ra.D;
+    RUN(c, name, 0.0, bytes, rollout_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
+  }
+  return DBSDE_OK;
 }
 
 int prep_weights(dbsde_ctx* c, const float* params);
@@ -965,7 +1033,8 @@ int forward_and_inputgrad(dbsde_ctx* c, int R, int Rp, bool need_u_only_and_z_st
     if (rc) return rc;
   }
   RUN(c, "rowdot_u", 2.0 * R * L[K + 1], 4.0 * R * L[K + 1],
-      rowdot_kernel<<<Rp / 16, 256, 0, c->stream>>>(c->H + c->col[K], S, c->Wp[K], c->wout, c->bout, c->u, Rp));
+      rowdot_kernel<<<Rp / 16, 256, 0, c->stream>>>(c->H + c->col[K], S, c->Wp[K], c->wout, c->bout, c->u, Rp,
+                                                   c->u_clamp ? c->umask : nullptr));
   for (int j = K; j >= 1; --j) {
     ChainArgs a = base_args(c);
     a.A = c->Delta + c->col[j];
@@ -1014,6 +1083,7 @@ int validate_batch(dbsde_ctx* c, const dbsde_batch* b) {
   if (!b->Xi) return fail(c, DBSDE_EINVAL, "Xi is NULL");
   if (b->xi_rows != 1 && b->xi_rows != b->M) return fail(c, DBSDE_EINVAL, "Xi must have 1 or M rows");
   if (b->W && !b->t) return fail(c, DBSDE_EINVAL, "t is required with W");
+  if (b->path0 < 0 || b->path0 + b->M > (1LL << 32)) return fail(c, DBSDE_EINVAL, "path0 out of range");
   return DBSDE_OK;
 }
 
@@ -1023,13 +1093,38 @@ int nv_x(dbsde_ctx* c) {
   return nv;
 }
 
-FusedArgs fused_args(dbsde_ctx* c, int R, int N1) {
+CotanParams cotan_params(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
+  const dbsde_problem& pr = c->cfg.problem;
+  CotanParams p{};
+  p.R = R;
+  p.Rp = Rp;
+  p.N1 = N1;
+  p.D = c->D;
+  p.Dp = c->Dp;
+  p.gcols = c->gcols;
+  p.xin = c->xin;
+  p.sdw = c->sdw;
+  p.zfull = c->zfull;
+  p.u = c->u;
+  p.rowsum = c->rowsum;
+  p.q3S = q3 ? c->q3S : nullptr;
+  p.phi_r = pr.phi_r;
+  p.phi_c = pr.phi_c;
+  p.phi_zz = pr.phi_zz;
+  p.strike = pr.strike;
+  p.g_alpha = pr.g_alpha;
+  p.g_kind = pr.g_kind;
+  return p;
+}
+
+FusedArgs fused_args(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
   FusedArgs a;
   memset(&a, 0, sizeof(a));
   a.R = R;
   a.N1 = N1;
   a.D = c->D;
-  a.gcols = c->D;
+  a.gcols = c->gcols;
+  a.u_clamp = c->u_clamp;
   a.Dp = c->Dp;
   a.W = c->Wp[0];
   a.S = c->Stot;
@@ -1037,14 +1132,7 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int N1) {
   a.act = c->act;
   a.rho = c->rho;
   a.xin = c->xin;
-  a.BtIn = c->BtIn;
-  a.BtZ = c->BtZ;
-  a.ldz = c->Stot_x;
-  for (int j = 1; j <= c->K; ++j) {
-    a.Bf[j - 1] = c->Bf[j];
-    a.Bb[j - 1] = c->Bb[j];
-    a.beta[j - 1] = c->beta[j];
-  }
+  for (int j = 1; j <= c->K; ++j) a.beta[j - 1] = c->beta[j];
   a.wout = c->wout;
   a.bout = c->bout;
   a.Abuf = c->Abuf;
@@ -1055,16 +1143,18 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int N1) {
   a.zfull = c->zfull;
   a.rowsum = c->rowsum;
   a.sdw = c->sdw;
+  a.cp = cotan_params(c, R, Rp, N1, q3);
   a.zbar = c->zbar;
   a.ubar = c->ubar;
+  a.u16 = c->tnw ? nullptr : c->u16;
+  a.loss_part = c->loss_part;
   a.Hdot = c->Hdot;
   a.Alpha = c->Alpha;
-  // stage sequences of phaseA2 / phaseC2 (phase.hpp)
+  // stage sequences (phase.hpp): every image streamed as two pieces, input
+  // blocks [0, H) and [H, TI)
   const int TW = c->Wp[0] / 16, TDp = c->Dp / 16, K = c->K;
-  // phase3 streams every image as two pieces (input blocks [0, H) and [H, TI))
-  const bool pieces = c->phase_ver == 3;
   auto add = [&](const float** imgs, int* nfs, int& n, const float* img, int TO, int TI) {
-    if (!pieces || TI < 2) {
+    if (TI < 2) {
       imgs[n] = img;
       nfs[n++] = TO * TI;
       return;
@@ -1183,7 +1273,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   if (rc) return rc;
   HIPC(c, hipSetDevice(c->device));
   const int M = b->M, N = b->N, N1 = N + 1, D = c->D, K = c->K, S = c->Stot;
-  const int R = M * N1, Rp = (R + PH_ROWS - 1) / PH_ROWS * PH_ROWS;
+  const int R = M * N1, Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD;
   if ((rc = ensure_rows(c, Rp, N))) return rc;
   hipStream_t s = c->stream;
   const auto& L = c->L;
@@ -1195,27 +1285,9 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   // ---- rollout (network-independent: mu/sigma never read Y, Z)
   if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
   {
-    RolloutArgs ra{};
-    ra.M = M;
-    ra.N = N;
-    ra.D = D;
-    ra.ldx = c->Dp;
-    ra.t = b->t;
-    ra.W = b->W;
-    ra.Xi = b->Xi;
-    ra.xi_rows = b->xi_rows;
-    ra.T = c->cfg.T;
-    ra.seed = b->seed;
-    ra.offset = b->offset;
-    ra.path0 = b->path0;
-    ra.mu_a = pr.mu_a;
-    ra.sig_a = pr.sig_a;
-    ra.sig_b = pr.sig_b;
-    ra.xin = c->xin;
-    ra.sdw = c->sdw;
-    const int nthr = M * D;
-    RUN(c, "rollout", 6.0 * (double)M * N * D, 4.0 * (double)M * N * D * (b->W ? 4 : 3),
-        rollout_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
+    RolloutArgs ra = rollout_args(c, b);
+    ra.out = PATH_ROLLOUT;
+    if ((rc = launch_paths(c, ra))) return rc;
   }
   const bool q3 = pr.q3 && D == 1;
   if (q3) RUN(c, "q3_sum", 0.0, 4.0 * M * N, q3_sum_kernel<<<N, 256, 0, s>>>(c->sdw, c->Dp, M, N, c->q3S));
@@ -1225,40 +1297,21 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   FusedArgs fa;
   const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act) : -1;
   if (fv >= 0) {
-    fa = fused_args(c, R, N1);
+    fa = fused_args(c, R, Rp, N1, q3);
     const int nv = nv_x(c);
     const double flA = 2.0 * R * ((D + 1.0) * nv + 2.0 * K * L[1] * (double)L[1] + (double)nv * D);
     const double byA = 4.0 * R * (c->Dp + 4.0 * S + 8.0);
-    if (c->phase_ver == 1)
-      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / 64, 256, 0, s>>>(fa));
-    else if (c->phase_ver == 2)
-      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A2<<<Rp / PH_ROWS, 64 * PH_WAVES, 0, s>>>(fa));
-    else
-      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A3<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
-    CotanArgs ca{};
-    ca.R = R;
-    ca.Rp = Rp;
-    ca.N1 = N1;
-    ca.D = D;
-    ca.Dp = c->Dp;
-    ca.xin = c->xin;
-    ca.sdw = c->sdw;
-    ca.zfull = c->zfull;
-    ca.u = c->u;
-    ca.rowsum = c->rowsum;
-    ca.q3S = q3 ? c->q3S : nullptr;
-    ca.phi_r = pr.phi_r;
-    ca.phi_c = pr.phi_c;
-    ca.phi_zz = pr.phi_zz;
-    ca.strike = pr.strike;
-    ca.g_kind = pr.g_kind;
-    ca.zbar = c->zbar;
-    ca.ubar = c->ubar;
-    ca.u16 = c->u16;
-    ca.lossrow = c->lossrow;
-    ca.loss_part = c->loss_part;
-    RUN(c, "cotangent", 0.0, 4.0 * R * 5.0 * D, cotan_kernel<<<Rp / 16, 256, 0, s>>>(ca));
-    nloss_parts = Rp / 16;
+    RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+    if (grad) {
+      const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
+      const double byC = 4.0 * R * (4.0 * c->Dp + 5.0 * S);
+      RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+      nloss_parts = Rp / P3_ROWS;
+    } else {
+      RUN(c, "loss_rows", 0.0, 4.0 * R * 3.0 * D,
+          cotan_kernel<<<Rp / 16, 256, 0, s>>>(cotan_params(c, R, Rp, N1, q3), c->loss_part));
+      nloss_parts = Rp / 16;
+    }
   } else {
     if ((rc = forward_and_inputgrad(c, R, Rp, false))) return rc;
 
@@ -1274,11 +1327,14 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
       a.ldx = c->Dp;
       a.u = c->u;
       a.q3S = q3 ? c->q3S : nullptr;
+      a.umask = c->u_clamp ? c->umask : nullptr;
       a.phi_r = pr.phi_r;
       a.phi_c = pr.phi_c;
       a.phi_zz = pr.phi_zz;
       a.strike = pr.strike;
+      a.g_alpha = pr.g_alpha;
       a.g_kind = pr.g_kind;
+      a.gcols = c->gcols;
       a.zbar = c->zbar;
       a.rres = c->rres;
       a.lossrow = c->lossrow;
@@ -1288,31 +1344,19 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     }
     RUN(c, "ubar_loss", 0.0, 16.0 * R,
         ubar_kernel<<<Rp / 256 + 1, 256, 0, s>>>(c->rres, c->xin, c->Dp, R, Rp, N1, pr.phi_r, c->lossrow, c->ubar,
-                                                 c->u16, c->loss_part));
+                                                 c->u16, c->loss_part, c->u_clamp ? c->umask : nullptr));
     nloss_parts = Rp / 256 + 1;
   }
   float* loss_dst = (out && out->loss) ? out->loss : c->loss_tmp;
-  // loss sum and gradient clear run beside phase C
+  // the loss sum runs beside the weight-gradient kernels
   if ((rc = fork_side(c, 1, [&]() {
-         hipStream_t ss = c->stream;
-         RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, ss>>>(c->loss_part, nloss_parts, loss_dst));
-         if (grad) HIPC(c, hipMemsetAsync(grad, 0, (size_t)c->nparams * 4, ss));
+         RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, c->stream>>>(c->loss_part, nloss_parts, loss_dst));
          return DBSDE_OK;
        })))
     return rc;
 
   if (grad) {
-    if (fv >= 0) {
-      const int nv = nv_x(c);
-      const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
-      const double byC = 4.0 * R * (c->Dp + 5.0 * S);
-      if (c->phase_ver == 1)
-        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / 64, 256, 0, s>>>(fa));
-      else if (c->phase_ver == 2)
-        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C2<<<Rp / PH_ROWS, 64 * PH_WAVES, 0, s>>>(fa));
-      else
-        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C3<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
-    } else {
+    if (fv < 0) {
       // ---- forward tangent along zbar
       {
         ChainArgs a = base_args(c);
@@ -1387,8 +1431,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
           return rc;
       }
     }
-    // ---- parameter gradients (grad cleared on the side stream)
-    if ((rc = join_side(c, 1))) return rc;
+    // ---- parameter gradients
     if (c->tnw) {
       if ((rc = launch_tnw(c, R, Rp))) return rc;
       if ((rc = finalize_grads(c, params, grad))) return rc;
@@ -1487,7 +1530,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
         export_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, out->X,
                                                                   out->Y, out->Z));
   }
-  if (!grad && (rc = join_side(c, 1))) return rc;
+  if ((rc = join_side(c, 1))) return rc;
   return DBSDE_OK;
 }
 
@@ -1495,7 +1538,7 @@ int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const 
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
   if (!params || !t || !X || R < 1) return fail(c, DBSDE_EINVAL, "bad net_u arguments");
   HIPC(c, hipSetDevice(c->device));
-  const int Rp = (R + PH_ROWS - 1) / PH_ROWS * PH_ROWS, D = c->D;
+  const int Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD, D = c->D;
   int rc;
   if ((rc = ensure_rows(c, Rp, 1))) return rc;
   hipStream_t s = c->stream;
@@ -1520,12 +1563,16 @@ int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const 
 int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, float* v, const dbsde_optim* o) {
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
   if (!params || !grad || !o) return fail(c, DBSDE_EINVAL, "bad optimizer arguments");
-  if (o->kind < 0 || o->kind > 2) return fail(c, DBSDE_EINVAL, "unknown optimizer kind");
-  if (o->kind != DBSDE_OPT_SGD && (!m || !v)) return fail(c, DBSDE_EINVAL, "Adam needs m and v");
+  if (o->kind < DBSDE_OPT_ADAM || o->kind > DBSDE_OPT_ASGD) return fail(c, DBSDE_EINVAL, "unknown optimizer kind");
+  const bool needs_m = o->kind == DBSDE_OPT_ADAM || o->kind == DBSDE_OPT_ADAMW || o->kind == DBSDE_OPT_ADAMAX ||
+                       o->kind == DBSDE_OPT_ADADELTA || o->kind == DBSDE_OPT_ASGD;
+  const bool needs_v = o->kind != DBSDE_OPT_SGD && o->kind != DBSDE_OPT_ASGD;
+  if ((needs_m && !m) || (needs_v && !v)) return fail(c, DBSDE_EINVAL, "optimizer state buffer is NULL");
   if (o->step < 1) return fail(c, DBSDE_EINVAL, "step must be >= 1");
   HIPC(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const long long n = c->nparams;
+  // scalar factors in double, as torch.optim computes them in Python floats
   OptArgs a{};
   a.kind = o->kind;
   a.lr = o->lr;
@@ -1535,16 +1582,70 @@ int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, flo
   a.max_norm = o->max_norm;
   a.omb1 = (float)(1.0 - (double)o->beta1);
   a.omb2 = (float)(1.0 - (double)o->beta2);
-  const double bc1 = 1.0 - std::pow((double)o->beta1, (double)o->step);
-  const double bc2 = 1.0 - std::pow((double)o->beta2, (double)o->step);
+  const double t = (double)o->step;
+  const double bc1 = 1.0 - std::pow((double)o->beta1, t);
+  const double bc2 = 1.0 - std::pow((double)o->beta2, t);
   a.step_size = (float)((double)o->lr / bc1);
   a.bc2_sqrt = (float)std::sqrt(bc2);
+  a.alpha = o->alpha;
+  a.rho = o->rho;
+  if (o->kind == DBSDE_OPT_RMSPROP) a.omb2 = (float)(1.0 - (double)o->alpha);
+  if (o->kind == DBSDE_OPT_ADADELTA) a.omb2 = (float)(1.0 - (double)o->rho);
+  if (o->kind == DBSDE_OPT_ADAGRAD) a.step_size = (float)((double)o->lr / (1.0 + (t - 1.0) * (double)o->lr_decay));
+  if (o->kind == DBSDE_OPT_ASGD) {
+    a.asgd_eta = o->asgd_eta;
+    a.asgd_decay = (float)(1.0 - (double)o->lambd * (double)o->asgd_eta);
+    a.asgd_mu = o->asgd_mu;
+    a.asgd_copy = o->asgd_mu == 1.f;
+  }
+  a.loss = o->loss;
   a.nparts = c->opt_nparts;
   if (o->max_norm > 0.f)
     RUN(c, "grad_sqnorm", 2.0 * n, 4.0 * n, sqnorm_kernel<<<c->opt_nparts, 256, 0, s>>>(grad, c->d_used, n, c->opt_part));
   RUN(c, "optimizer", 10.0 * n, 24.0 * n,
       optim_kernel<<<256, 256, 0, s>>>(params, grad, m, v, c->d_used, n, c->opt_part, a));
   return DBSDE_OK;
+}
+
+int dbsde_brownian_dim(const dbsde_ctx* c) { return c ? c->nb : -1; }
+
+int dbsde_set_corr(dbsde_ctx* c, const float* L, int n) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  HIPC(c, hipSetDevice(c->device));
+  if (!L) {
+    if (c->Lt) {
+      HIPC(c, hipStreamSynchronize(c->stream));
+      (void)hipFree(c->Lt);
+      c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), (void*)c->Lt));
+      c->Lt = nullptr;
+    }
+    return DBSDE_OK;
+  }
+  if (c->heston) return fail(c, DBSDE_EINVAL, "dbsde_set_corr: correlated increments are for DIAG problems");
+  if (n != c->nb) return fail(c, DBSDE_EINVAL, "dbsde_set_corr: L must be [nb, nb], nb = the Brownian dimension");
+  if (n > CP_NBMAX) return fail(c, DBSDE_EINVAL, "dbsde_set_corr: Brownian dimension > 128 is not supported");
+  std::vector<float> lt((size_t)n * n, 0.f);
+  for (int d = 0; d < n; ++d)
+    for (int k = 0; k <= d; ++k) lt[(size_t)k * n + d] = L[(size_t)d * n + k];   // L^T, lower part of L only
+  int rc;
+  if (!c->Lt && (rc = dalloc_t(c, &c->Lt, (size_t)n * n))) return rc;
+  HIPC(c, hipStreamSynchronize(c->stream));
+  HIPC(c, hipMemcpy(c->Lt, lt.data(), lt.size() * sizeof(float), hipMemcpyHostToDevice));
+  return DBSDE_OK;
+}
+
+int dbsde_brownian(dbsde_ctx* c, const dbsde_batch* b, float* t, float* W, int increments) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  int rc = validate_batch(c, b);
+  if (rc) return rc;
+  if (b->W || b->t) return fail(c, DBSDE_EINVAL, "dbsde_brownian draws a device-mode batch (W and t must be NULL)");
+  if (!t || !W) return fail(c, DBSDE_EINVAL, "t and W outputs are required");
+  HIPC(c, hipSetDevice(c->device));
+  RolloutArgs ra = rollout_args(c, b);
+  ra.out = increments ? PATH_FETCH_DW : PATH_FETCH_W;
+  ra.t_out = t;
+  ra.W_out = W;
+  return launch_paths(c, ra);
 }
 
 int dbsde_profile_enable(dbsde_ctx* c, int enable) {

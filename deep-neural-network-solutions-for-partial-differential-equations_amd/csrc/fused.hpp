@@ -1,18 +1,6 @@
-// fused.hpp -- wave-level fused phase kernels (gfx950).
-//
-// One wavefront owns 16 consecutive rows (= 16 (path, time) pairs) and pushes
-// them through every layer of a phase without leaving the CU:
-//   phaseA : forward (a_j, h_j, u) + input gradient (delta_j, g_j, Z) + the
-//            per-row sums the residual needs
-//   phaseC : forward tangent along zbar (adot_j, hdot_j) + reverse (p_j, alpha_j)
-// Activations stay in registers in the MFMA accumulator layout
-//   acc[t][jj] = M[row 4q+jj][col 16t+cl]   (q = lane>>4, cl = lane&15)
-// and are re-laid out for the next layer's A operand through a per-wave LDS
-// tile read back as float4 (row cl, k = 16c+4q..+3).  Weight fragments are
-// read straight from global memory (L2-resident, shared by every wave) one
-// 16-deep K chunk ahead.  No workgroup barrier anywhere: a workgroup is one
-// wave.  Only what later kernels need is written to HBM (a, h, g, delta in
-// phase A; hdot, alpha in phase C).
+// fused.hpp -- shared pieces of the fused phase kernels (phase.hpp): their
+// argument block, register tiles, compile-time activations, and the closed-form
+// residual / cotangent of one row (DeepBSDE.py:223-240 restated).
 #pragma once
 #include <type_traits>
 
@@ -20,28 +8,41 @@
 
 namespace dbsde {
 
+// residual / cotangent inputs, shared by phase C (fused) and the forward-only
+// loss kernel
+struct CotanParams {
+  int R, Rp, N1, D, Dp, gcols;
+  const float* xin;         // [Rp, Dp]  [t, X, 1, 0..]
+  const float* sdw;         // [Rp, Dp]  sigma dW (cols 1..D)
+  const float* zfull;       // [Rp, Dp]  Z (cols 1..D)
+  const float* u;           // [Rp]      Y
+  const float* rowsum;      // [Rp, 8]   [s_zs, s_xz, s_zz, s_x, s_xx, z_1, u-mask, 0]
+  const float* q3S;         // [N] or null
+  float phi_r, phi_c, phi_zz, strike, g_alpha;
+  int g_kind;
+};
+
 struct FusedArgs {
   int R, N1, D, Dp, W, S;   // rows, N+1, D, padded D, padded level width, level stride
   int has_v, act;
   int gcols;                // leading state columns entering g (row sums s_x, s_xx)
+  int u_clamp;              // u = max(net, 0) (heston_dnnpde.py:568)
   float rho;
   const float* xin;         // [Rp, Dp]
-  const float* BtIn;        // [Stot_x, Dp]
-  const float* BtZ;         // [Dp, Stot_x]
-  int ldz;                  // Stot_x
-  const float* Bf[7];       // block j (1..K): [W, W]  (Bt for a_j = h_j B_j^T)
-  const float* Bb[7];       // block j: [W, W] = B_j^T (Bt for g_j = delta_j B_j)
   const float* beta[7];     // FC/Resnet level-j bias
   const float* wout;
   const float* bout;
   // phase A outputs
   float *Abuf, *H, *G, *Delta, *u, *zfull, *rowsum;  // rowsum [Rp, 8]
   const float* sdw;         // [Rp, Dp]
-  // phase C
-  const float* zbar;        // [Rp, Dp]
-  const float* ubar;        // [Rp]
+  // phase C: cotangents (computed in its prologue) and outputs
+  CotanParams cp;
+  float* zbar;              // [Rp, Dp] (written for the weight-gradient kernel)
+  float* ubar;              // [Rp]
+  float* u16;               // [Rp, 16] col 0 = ubar (split-K weight-gradient path) or null
+  double* loss_part;        // [Rp / 64] per-workgroup loss sums
   float *Hdot, *Alpha;
-  // phase.hpp kernels: fragment images of the stage sequence of each pass
+  // fragment images of the stage sequence of each pass (phase.hpp)
   const float* simgA[32];
   int snfA[32];
   int nA;
@@ -56,14 +57,9 @@ struct Mat {
 };
 
 // activation with compile-time kind: value + first derivative, and first +
-// second derivative (one sincosf / tanhf per element)
+// second derivative (one sincos / tanh per element)
 template <int ACT>
 __device__ __forceinline__ void act_v1(float a, float& f, float& d1) {
-#ifdef DBSDE_EXP_CHEAPACT
-  f = a;   // timing experiment only: no transcendental epilogue
-  d1 = 1.f;
-  return;
-#endif
   if constexpr (ACT == ACT_SINE) {
     fast_sincosf(a, f, d1);
   } else if constexpr (ACT == ACT_TANH) {
@@ -76,9 +72,6 @@ __device__ __forceinline__ void act_v1(float a, float& f, float& d1) {
 }
 template <int ACT>
 __device__ __forceinline__ float act_1(float a) {
-#ifdef DBSDE_EXP_CHEAPACT
-  return a;
-#endif
   if constexpr (ACT == ACT_SINE) {
     float sv, cv;
     fast_sincosf(a, sv, cv);
@@ -92,11 +85,6 @@ __device__ __forceinline__ float act_1(float a) {
 }
 template <int ACT>
 __device__ __forceinline__ void act_12(float a, float& d1, float& d2) {
-#ifdef DBSDE_EXP_CHEAPACT
-  d1 = a;
-  d2 = 1.f;
-  return;
-#endif
   if constexpr (ACT == ACT_SINE) {
     float sv;
     fast_sincosf(a, sv, d1);
@@ -124,411 +112,15 @@ struct SFor {
   }
 };
 
-// acc += A(LDS, 16 x K, row stride lda) * Bt(global, rows = output cols)^T
-template <int TO>
-__device__ __forceinline__ void wave_gemm(Mat<TO>& acc, const float* Al, int lda, int K, const float* Bt, int ldb,
-                                          int kofs) {
-  const int lane = threadIdx.x & 63, cl = lane & 15, q = lane >> 4;
-  const float* bp = Bt + (size_t)cl * ldb + kofs + 4 * q;
-  const float* ap = Al + cl * lda + 4 * q;
-  const int nc = K >> 4;
-  floatx4 b0[TO], b1[TO];
-#pragma unroll
-  for (int t = 0; t < TO; ++t) b0[t] = *(const floatx4*)(bp + (size_t)16 * t * ldb);
-  int c = 0;
-  for (; c + 2 <= nc; c += 2) {
-#pragma unroll
-    for (int t = 0; t < TO; ++t) b1[t] = *(const floatx4*)(bp + (size_t)16 * t * ldb + 16 * (c + 1));
-    {
-      const floatx4 a = *(const floatx4*)(ap + 16 * c);
-#pragma unroll
-      for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.x, b0[t].x, acc.v[t]);
-#pragma unroll
-      for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.y, b0[t].y, acc.v[t]);
-#pragma unroll
-      for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.z, b0[t].z, acc.v[t]);
-#pragma unroll
-      for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.w, b0[t].w, acc.v[t]);
-    }
-    if (c + 2 < nc) {
-#pragma unroll
-      for (int t = 0; t < TO; ++t) b0[t] = *(const floatx4*)(bp + (size_t)16 * t * ldb + 16 * (c + 2));
-    }
-    {
-      const floatx4 a = *(const floatx4*)(ap + 16 * (c + 1));
-#pragma unroll
-      for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.x, b1[t].x, acc.v[t]);
-#pragma unroll
-      for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.y, b1[t].y, acc.v[t]);
-#pragma unroll
-      for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.z, b1[t].z, acc.v[t]);
-#pragma unroll
-      for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.w, b1[t].w, acc.v[t]);
-    }
-  }
-  if (c < nc) {  // odd chunk count: b0 holds chunk c
-    const floatx4 a = *(const floatx4*)(ap + 16 * c);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.x, b0[t].x, acc.v[t]);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.y, b0[t].y, acc.v[t]);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.z, b0[t].z, acc.v[t]);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.w, b0[t].w, acc.v[t]);
-  }
-}
-
-// Workgroup-cooperative variant: the 4 waves of a workgroup (64 rows) share
-// each 16-deep chunk of Bt through a double-buffered LDS stage (Bs holds
-// 2 x [16*TO][FB_LS] floats); A stays per wave.  Every wave must call it.
-constexpr int FB_LS = 24;   // = 8 mod 16: conflict-free ds_read_b128 fragment reads (gfx950 lane groups)
-template <int TO>
-__device__ __forceinline__ void wg_gemm(Mat<TO>& acc, const float* Al, int lda, int K, const float* Bt, int ldb,
-                                        int kofs, float* Bs) {
-  const int tid = threadIdx.x, lane = tid & 63, cl = lane & 15, q = lane >> 4;
-  constexpr int NB4 = 16 * TO * 4;            // float4 per chunk
-  constexpr int NL = (NB4 + 255) / 256;       // per thread
-  constexpr int BUF = 16 * TO * FB_LS;
-  const int nc = K >> 4;
-  floatx4 st[NL];
-  auto gl = [&](int c) {
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int idx = tid + 256 * i;
-      if (idx < NB4) st[i] = *(const floatx4*)(Bt + (size_t)(idx >> 2) * ldb + kofs + 16 * c + 4 * (idx & 3));
-    }
-  };
-  auto ls = [&](int b) {
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int idx = tid + 256 * i;
-      if (idx < NB4) *(floatx4*)(Bs + b * BUF + (idx >> 2) * FB_LS + 4 * (idx & 3)) = st[i];
-    }
-  };
-  gl(0);
-  ls(0);
-  __syncthreads();
-  const float* ap = Al + cl * lda + 4 * q;
-  for (int c = 0; c < nc; ++c) {
-#ifdef DBSDE_EXP_NOBSTAGE
-    const int b = 0;   // timing experiment only: reuse chunk 0, no staging, no barrier
-#else
-    const int b = c & 1;
-    if (c + 1 < nc) gl(c + 1);
-#endif
-    const floatx4 a = *(const floatx4*)(ap + 16 * c);
-    floatx4 bv[TO];
-#pragma unroll
-    for (int t = 0; t < TO; ++t) bv[t] = *(const floatx4*)(Bs + b * BUF + (16 * t + cl) * FB_LS + 4 * q);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.x, bv[t].x, acc.v[t]);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.y, bv[t].y, acc.v[t]);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.z, bv[t].z, acc.v[t]);
-#pragma unroll
-    for (int t = 0; t < TO; ++t) acc.v[t] = mfma4(a.w, bv[t].w, acc.v[t]);
-#ifndef DBSDE_EXP_NOBSTAGE
-    if (c + 1 < nc) ls(b ^ 1);
-    __syncthreads();
-#endif
-  }
-}
-
 template <int TT>
 __device__ __forceinline__ void zero(Mat<TT>& m) {
 #pragma unroll
   for (int t = 0; t < TT; ++t) m.v[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 }
 
-// accumulator-layout tile <-> global row-major matrix
-template <int TT>
-__device__ __forceinline__ void gstore(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
-#ifdef DBSDE_EXP_NOSTORE
-  if (base != nullptr) return;   // timing experiment only: activation stores dropped
-#endif
-  const int lane = threadIdx.x & 63, cl = lane & 15, q = lane >> 4;
-#pragma unroll
-  for (int t = 0; t < TT; ++t)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) base[(size_t)(row0 + 4 * q + jj) * ld + col0 + 16 * t + cl] = m.v[t][jj];
-}
-template <int TT>
-__device__ __forceinline__ void gload(Mat<TT>& m, const float* base, int ld, int row0, int col0) {
-  const int lane = threadIdx.x & 63, cl = lane & 15, q = lane >> 4;
-#pragma unroll
-  for (int t = 0; t < TT; ++t)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) m.v[t][jj] = base[(size_t)(row0 + 4 * q + jj) * ld + col0 + 16 * t + cl];
-}
-// accumulator-layout tile -> LDS row-major (the next layer's A operand)
-template <int TT>
-__device__ __forceinline__ void lstore(const Mat<TT>& m, float* L, int ld) {
-  const int lane = threadIdx.x & 63, cl = lane & 15, q = lane >> 4;
-#pragma unroll
-  for (int t = 0; t < TT; ++t)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) L[(4 * q + jj) * ld + 16 * t + cl] = m.v[t][jj];
-}
-// 16 global rows -> LDS rows (float4 copies)
-__device__ __forceinline__ void rows_to_lds(const float* src, int lds_src, int row0, int ncols, float* L, int ld) {
-  const int lane = threadIdx.x & 63;
-  const int n4 = ncols >> 2;
-  for (int i = lane; i < 16 * n4; i += 64) {
-    const int r = i / n4, c = (i - r * n4) * 4;
-    *(floatx4*)(L + r * ld + c) = *(const floatx4*)(src + (size_t)(row0 + r) * lds_src + c);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// phase A: forward + input gradient + Z (+ residual row sums)
-// ---------------------------------------------------------------------------
-template <int T, int TD, int K, int ACT>
-__global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
-  constexpr int LDX = TD * 16 + 4, LDT = T * 16 + 4;
-  constexpr int TB = T > TD ? T : TD;
-  __shared__ float Bs[2 * 16 * TB * FB_LS];
-  __shared__ float Xall[4 * 16 * LDX];
-  __shared__ float Tall[4 * 16 * LDT];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cl = lane & 15, q = lane >> 4;
-  float* Xl = Xall + wave * 16 * LDX;
-  float* Tl = Tall + wave * 16 * LDT;
-  const int row0 = blockIdx.x * 64 + wave * 16;
-  const int Wd = p.W, S = p.S;
-  rows_to_lds(p.xin, p.Dp, row0, p.Dp, Xl, LDX);
-  __builtin_amdgcn_s_waitcnt(0);
-
-  Mat<T> s1[K + 1];   // act'(a_j)
-  Mat<T> h, acc;
-  // level 0
-  zero(acc);
-  wg_gemm<T>(acc, Xl, LDX, p.Dp, p.BtIn, p.Dp, 0, Bs);
-  gstore(acc, p.Abuf, S, row0, 0);
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      float f, d;
-      act_v1<ACT>(acc.v[t][jj], f, d);
-      h.v[t][jj] = f;
-      s1[0].v[t][jj] = d;
-    }
-  gstore(h, p.H, S, row0, 0);
-  lstore(h, Tl, LDT);
-  SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
-    constexpr int j = decltype(jc)::value;
-    zero(acc);
-    wg_gemm<T>(acc, Tl, LDT, Wd, p.Bf[j - 1], Wd, 0, Bs);
-    if (p.has_v) wg_gemm<T>(acc, Xl, LDX, p.Dp, p.BtIn + (size_t)j * Wd * p.Dp, p.Dp, 0, Bs);
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const float bb = p.has_v ? 0.f : p.beta[j - 1][16 * t + cl];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const float a = acc.v[t][jj] + bb;
-        acc.v[t][jj] = a;
-        float f, d;
-        act_v1<ACT>(a, f, d);
-        s1[j].v[t][jj] = d;
-        h.v[t][jj] = f + p.rho * h.v[t][jj];
-      }
-    }
-    gstore(acc, p.Abuf, S, row0, j * Wd);
-    gstore(h, p.H, S, row0, j * Wd);
-    if (j < K) lstore(h, Tl, LDT);
-  });
-  // u = h_{K+1} . w_out + b_out
-  {
-    float us[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const float w = p.wout[16 * t + cl];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) us[jj] += h.v[t][jj] * w;
-    }
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const float s = red16(us[jj]);
-      if (cl == 0) p.u[row0 + 4 * q + jj] = s + p.bout[0];
-    }
-  }
-  // input gradient: g_{K+1} = w_out, delta_K = w_out act'(a_K)
-  Mat<T> g;
-  Mat<TD> z;
-  zero(z);
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const float w = p.wout[16 * t + cl];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      g.v[t][jj] = w;
-      acc.v[t][jj] = w * s1[K].v[t][jj];
-    }
-  }
-  gstore(acc, p.Delta, S, row0, K * Wd);
-  lstore(acc, Tl, LDT);
-  SFor<0, K>::run([&](auto ic) __attribute__((always_inline)) {
-    constexpr int j = K - decltype(ic)::value;
-    if (p.has_v) wg_gemm<TD>(z, Tl, LDT, Wd, p.BtZ, p.ldz, j * Wd, Bs);   // Z += delta_j V_j
-    Mat<T> gn;
-    zero(gn);
-    wg_gemm<T>(gn, Tl, LDT, Wd, p.Bb[j - 1], Wd, 0, Bs);                 // delta_j B_j
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const float gv = gn.v[t][jj] + p.rho * g.v[t][jj];
-        g.v[t][jj] = gv;
-        acc.v[t][jj] = gv * s1[j - 1].v[t][jj];
-      }
-    gstore(g, p.G, S, row0, (j - 1) * Wd);
-    gstore(acc, p.Delta, S, row0, (j - 1) * Wd);
-    lstore(acc, Tl, LDT);
-  });
-  wg_gemm<TD>(z, Tl, LDT, Wd, p.BtZ, p.ldz, 0, Bs);                      // Z += delta_0 W_in
-  // Z out + residual row sums: [s_zs, s_xz, s_zz, s_x, s_xx, z1]
-  gstore(z, p.zfull, p.Dp, row0, 0);
-  const int D = p.D;
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    const int r = row0 + 4 * q + jj;
-    const float* sr = p.sdw + (size_t)r * p.Dp;
-    float s_zs = 0.f, s_xz = 0.f, s_zz = 0.f, s_x = 0.f, s_xx = 0.f, z1 = 0.f;
-#pragma unroll
-    for (int t = 0; t < TD; ++t) {
-      const int c = 16 * t + cl;
-      const float zv = z.v[t][jj];
-      if (c >= 1 && c <= D) {
-        const float xv = Xl[(4 * q + jj) * LDX + c];
-        s_zs += zv * sr[c];
-        s_xz += xv * zv;
-        s_zz += zv * zv;
-        s_x += xv;
-        s_xx += xv * xv;
-      }
-      if (c == 1) z1 = zv;
-    }
-    s_zs = red16(s_zs);
-    s_xz = red16(s_xz);
-    s_zz = red16(s_zz);
-    s_x = red16(s_x);
-    s_xx = red16(s_xx);
-    z1 = red16(z1);
-    if (cl == 0) {
-      float* o = p.rowsum + (size_t)r * 8;
-      o[0] = s_zs;
-      o[1] = s_xz;
-      o[2] = s_zz;
-      o[3] = s_x;
-      o[4] = s_xx;
-      o[5] = z1;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// phase C: forward tangent along zbar + reverse over (primal, tangent)
-// ---------------------------------------------------------------------------
-template <int T, int TD, int K, int ACT>
-__global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
-  constexpr int LDX = TD * 16 + 4, LDT = T * 16 + 4;
-  constexpr int TB = T > TD ? T : TD;
-  __shared__ float Bs[2 * 16 * TB * FB_LS];
-  __shared__ float Zall[4 * 16 * LDX];
-  __shared__ float Tall[4 * 16 * LDT];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, cl = lane & 15, q = lane >> 4;
-  float* Zl = Zall + wave * 16 * LDX;
-  float* Tl = Tall + wave * 16 * LDT;
-  const int row0 = blockIdx.x * 64 + wave * 16;
-  const int Wd = p.W, S = p.S;
-  rows_to_lds(p.zbar, p.Dp, row0, p.Dp, Zl, LDX);
-  __builtin_amdgcn_s_waitcnt(0);
-
-  Mat<T> ad[K + 1];   // adot_j
-  Mat<T> hd, av;
-  // tangent level 0
-  zero(ad[0]);
-  wg_gemm<T>(ad[0], Zl, LDX, p.Dp, p.BtIn, p.Dp, 0, Bs);
-  gload(av, p.Abuf, S, row0, 0);
-#pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) hd.v[t][jj] = act_1<ACT>(av.v[t][jj]) * ad[0].v[t][jj];
-  gstore(hd, p.Hdot, S, row0, 0);
-  lstore(hd, Tl, LDT);
-  SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
-    constexpr int j = decltype(jc)::value;
-    zero(ad[j]);
-    wg_gemm<T>(ad[j], Tl, LDT, Wd, p.Bf[j - 1], Wd, 0, Bs);
-    if (p.has_v) wg_gemm<T>(ad[j], Zl, LDX, p.Dp, p.BtIn + (size_t)j * Wd * p.Dp, p.Dp, 0, Bs);
-    gload(av, p.Abuf, S, row0, j * Wd);
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        hd.v[t][jj] = act_1<ACT>(av.v[t][jj]) * ad[j].v[t][jj] + p.rho * hd.v[t][jj];
-    gstore(hd, p.Hdot, S, row0, j * Wd);
-    if (j < K) lstore(hd, Tl, LDT);
-  });
-  // reverse: p_{K+1} = ubar w_out ; alpha_K = w_out (ubar act'(a_K) + adot_K act''(a_K))
-  Mat<T> pv, al;
-  float ub[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) ub[jj] = p.ubar[row0 + 4 * q + jj];
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const float w = p.wout[16 * t + cl];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const float a = p.Abuf[(size_t)(row0 + 4 * q + jj) * S + K * Wd + 16 * t + cl];
-      float d1, d2;
-      act_12<ACT>(a, d1, d2);
-      pv.v[t][jj] = ub[jj] * w;
-      al.v[t][jj] = w * (ub[jj] * d1 + ad[K].v[t][jj] * d2);
-    }
-  }
-  gstore(al, p.Alpha, S, row0, K * Wd);
-  lstore(al, Tl, LDT);
-  SFor<0, K>::run([&](auto ic) __attribute__((always_inline)) {
-    constexpr int j = K - decltype(ic)::value;
-    zero(al);
-    wg_gemm<T>(al, Tl, LDT, Wd, p.Bb[j - 1], Wd, 0, Bs);   // alpha_j B_j
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const size_t o = (size_t)(row0 + 4 * q + jj) * S + (j - 1) * Wd + 16 * t + cl;
-        const float pp = al.v[t][jj] + p.rho * pv.v[t][jj];
-        pv.v[t][jj] = pp;
-        float d1, d2;
-        act_12<ACT>(p.Abuf[o], d1, d2);
-        al.v[t][jj] = pp * d1 + p.G[o] * ad[j - 1].v[t][jj] * d2;
-      }
-    gstore(al, p.Alpha, S, row0, (j - 1) * Wd);
-    if (j > 1) lstore(al, Tl, LDT);
-  });
-}
-
-// residuals, ubar, zbar and loss rows from phase A's row sums.
-// 16 threads per row (d-parallel zbar), 16 rows per 256-thread block.
-struct CotanArgs {
-  int R, Rp, N1, D, Dp;
-  const float* xin;
-  const float* sdw;
-  const float* zfull;
-  const float* u;
-  const float* rowsum;
-  const float* q3S;
-  float phi_r, phi_c, phi_zz, strike;
-  int g_kind;
-  float *zbar, *ubar, *u16, *lossrow;
-  double* loss_part;
-};
-
-// residual of row r (n < N: Y_{n+1} - Ytilde_{n+1}; n == N: Y_N - g(X_N)) and,
-// for terminal rows, the grad-g scale
-__device__ __forceinline__ float row_residual(const CotanArgs& p, int r, int n, float& gsc) {
+// residual of row r (n < N: Y_{n+1} - Ytilde_{n+1}, DeepBSDE.py:223-228;
+// n == N: Y_N - g(X_N), :232) and, for terminal rows, the grad-g scale
+__device__ __forceinline__ float row_residual(const CotanParams& p, int r, int n, float& gsc) {
   const float* rs = p.rowsum + (size_t)r * 8;
   const float y = p.u[r];
   gsc = 0.f;
@@ -538,83 +130,71 @@ __device__ __forceinline__ float row_residual(const CotanArgs& p, int r, int n, 
     const float phi = p.phi_r * (y - p.phi_c * rs[1]) + p.phi_zz * rs[2];
     return p.u[r + 1] - (y + phi * dt + zs);
   }
-  float g;
-  if (p.g_kind == 0) {
-    g = rs[4];
-  } else if (p.g_kind == 1) {
-    const float v = rs[3] - p.strike;
-    g = v > 0.f ? v : 0.f;
-    gsc = v > 0.f ? 1.f : 0.f;
-  } else if (p.g_kind == 2) {
-    const float v = rs[3] / (float)p.D - p.strike;
-    g = v > 0.f ? v : 0.f;
-    gsc = v > 0.f ? 1.f / (float)p.D : 0.f;
-  } else {
-    const float qv = 0.5f + 0.5f * rs[4];
-    g = logf(qv);
-    gsc = 1.f / qv;
-  }
-  return y - g;
+  return y - terminal_g(p.g_kind, rs[3], rs[4], p.gcols, p.strike, p.g_alpha, gsc);
 }
 
-__global__ void __launch_bounds__(256) cotan_kernel(CotanArgs p) {
+// cotangents of row r: ubar (d loss / d Y_r) and the per-row scalars the zbar
+// entries need.  The loss of the row is res^2 + |Z - grad g|^2 (terminal).
+struct RowCotan {
+  bool valid, term;
+  int n;
+  float res, ub, coefY, dt, gsc, mask, q3s;
+};
+__device__ __forceinline__ RowCotan row_cotan(const CotanParams& p, int r) {
+  RowCotan c{};
+  c.valid = r < p.R;
+  if (!c.valid) return c;
+  c.n = r % p.N1;
+  c.term = c.n == p.N1 - 1;
+  c.res = row_residual(p, r, c.n, c.gsc);
+  c.mask = p.rowsum[(size_t)r * 8 + 6];
+  if (c.term) {
+    c.ub = 2.f * c.res;
+  } else {
+    c.dt = p.xin[(size_t)(r + 1) * p.Dp] - p.xin[(size_t)r * p.Dp];
+    c.ub = -2.f * c.res * (1.f + p.phi_r * c.dt);
+    c.q3s = p.q3S ? p.q3S[c.n] : 0.f;
+  }
+  if (c.n >= 1) {
+    float g2;
+    c.ub += 2.f * row_residual(p, r - 1, c.n - 1, g2);
+  }
+  c.ub *= c.mask;
+  c.coefY = -2.f * c.res;
+  return c;
+}
+// zbar of column col (1 <= col <= D) from x, z, (sigma dW) of that column;
+// tz accumulates the terminal |Z - grad g|^2 over the g columns
+__device__ __forceinline__ float col_zbar(const CotanParams& p, const RowCotan& c, int col, float xv, float zv,
+                                          float sv, float& tz) {
+  if (!c.term) {
+    const float dphidz = -p.phi_r * p.phi_c * xv + 2.f * p.phi_zz * zv;
+    const float sd = p.q3S ? c.q3s : sv;
+    return c.mask * (c.coefY * (dphidz * c.dt + sd));
+  }
+  if (col > p.gcols) return 0.f;
+  const float e = zv - terminal_dg(p.g_kind, xv, c.gsc);
+  tz += e * e;
+  return c.mask * (2.f * e);
+}
+
+// Forward-only loss (predict / loss_function without backward): per-block
+// partial sums of the row losses; 16 threads per row, 16 rows per block.
+__global__ void __launch_bounds__(256) cotan_kernel(CotanParams p, double* loss_part) {
   const int sub = threadIdx.x & 15;
   const int r = blockIdx.x * 16 + (threadIdx.x >> 4);
   double lv = 0.0;
-  if (r < p.Rp) {
-    float* zb = p.zbar + (size_t)r * p.Dp;
-    if (r >= p.R) {
-      for (int c = sub; c < p.Dp; c += 16) zb[c] = 0.f;
-      if (sub == 0) {
-        p.ubar[r] = 0.f;
-        p.u16[(size_t)r * 16] = 0.f;
-      }
-    } else {
-      const int n = r % p.N1;
-      const bool term = n == p.N1 - 1;
-      float gsc;
-      const float res = row_residual(p, r, n, gsc);
-      float ub = term ? 2.f * res : -2.f * res;
-      if (!term) {
-        const float dt = p.xin[(size_t)(r + 1) * p.Dp] - p.xin[(size_t)r * p.Dp];
-        ub = -2.f * res * (1.f + p.phi_r * dt);
-      }
-      if (n >= 1) {
-        float g2;
-        ub += 2.f * row_residual(p, r - 1, n - 1, g2);
-      }
+  const RowCotan c = row_cotan(p, r);
+  if (c.valid) {
+    float tz = 0.f;
+    if (c.term) {
       const float* xr = p.xin + (size_t)r * p.Dp;
       const float* zr = p.zfull + (size_t)r * p.Dp;
       const float* sr = p.sdw + (size_t)r * p.Dp;
-      const float dt = term ? 0.f : p.xin[(size_t)(r + 1) * p.Dp] - xr[0];
-      const float coefY = -2.f * res;
-      float tz = 0.f;
-      for (int c = sub; c < p.Dp; c += 16) {
-        float v = 0.f;
-        if (c >= 1 && c <= p.D) {
-          const float xv = xr[c], zv = zr[c];
-          if (!term) {
-            const float dphidz = -p.phi_r * p.phi_c * xv + 2.f * p.phi_zz * zv;
-            const float sd = p.q3S ? p.q3S[n] : sr[c];
-            v = coefY * (dphidz * dt + sd);
-          } else {
-            const float dg = (p.g_kind == 0) ? 2.f * xv : (p.g_kind == 3 ? xv * gsc : gsc);
-            const float e = zv - dg;
-            tz += e * e;
-            v = 2.f * e;
-          }
-        }
-        zb[c] = v;
-      }
-      tz = red16(tz);
-      if (sub == 0) {
-        p.ubar[r] = ub;
-        p.u16[(size_t)r * 16] = ub;
-        const float l = res * res + tz;
-        p.lossrow[r] = l;
-        lv = (double)l;
-      }
+      for (int col = 1 + sub; col <= p.D; col += 16) (void)col_zbar(p, c, col, xr[col], zr[col], sr[col], tz);
     }
+    tz = red16(tz);
+    if (sub == 0) lv = (double)(c.res * c.res + tz);
   }
   __shared__ double red[256];
   red[threadIdx.x] = lv;
@@ -623,7 +203,7 @@ __global__ void __launch_bounds__(256) cotan_kernel(CotanArgs p) {
     if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) p.loss_part[blockIdx.x] = red[0];
+  if (threadIdx.x == 0) loss_part[blockIdx.x] = red[0];
 }
 
 }  // namespace dbsde

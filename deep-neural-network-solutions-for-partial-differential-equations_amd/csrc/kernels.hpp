@@ -104,141 +104,39 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 }
 
 // --------------------------------------------------------------------------
-// Philox4x32-10 + Box-Muller (device Brownian increments)
+// terminal condition g(X_N) over the leading G state columns and the scale of
+// its gradient (DeepBSDE.py:196-200 via autograd):
+//   0 sumsq   g = |x|^2                     dg = 2 x          (DeepBSDE.py:333-335)
+//   1 call    g = max(sum x - K, 0)         dg = gsc          (nd_BSPDE_case.py:521-522)
+//   2 basket  g = max(mean x - K, 0)        dg = gsc          (with_corr...py:577-579,
+//                                                              heston_dnnpde.py:550)
+//   3 log     g = log(1/2 + |x|^2/2)        dg = x gsc        (hjb_implement.py:597-598)
+//   4 smooth  g = a / (1 + e^{-alpha a}), a = mean x - K      (heston_dnnpde.py:551-556)
+// torch.maximum splits the gradient 1/2 : 1/2 at a tie, so gsc = 1/2 there.
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
-    uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
-    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
-    c[0] = n0;
-    c[1] = lo1;
-    c[2] = n2;
-    c[3] = lo0;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
+__device__ __forceinline__ float terminal_g(int kind, float s_x, float s_xx, int G, float strike, float alpha,
+                                            float& gsc) {
+  gsc = 0.f;
+  if (kind == 0) return s_xx;
+  if (kind == 1 || kind == 2) {
+    const float v = kind == 1 ? s_x - strike : s_x / (float)G - strike;
+    const float sc = kind == 1 ? 1.f : 1.f / (float)G;
+    gsc = v > 0.f ? sc : (v == 0.f ? 0.5f * sc : 0.f);
+    return v > 0.f ? v : 0.f;
   }
+  if (kind == 3) {
+    const float q = 0.5f + 0.5f * s_xx;
+    gsc = 1.f / q;
+    return logf(q);
+  }
+  const float a = s_x / (float)G - strike;
+  const float e = expf(-alpha * a);
+  const float den = 1.f + e;
+  gsc = (1.f / den + a * alpha * e / (den * den)) / (float)G;
+  return a / den;
 }
-
-// Four standard normals from one Philox4x32-10 block: both Box-Muller outputs
-// of the uniform pairs (c0, c1) and (c2, c3).  Counter = (d, n/4, m, offset),
-// key = seed: the stream is keyed by the global path index m, so sharding
-// paths over ranks reproduces the single-device increments.
-__device__ __forceinline__ void philox_normal4(unsigned long long seed, unsigned long long offset, uint32_t m,
-                                               uint32_t nq, uint32_t d, float z[4]) {
-  uint32_t c[4] = {d, nq, m, (uint32_t)offset};
-  philox4x32_10(c, (uint32_t)seed ^ (uint32_t)(offset >> 32), (uint32_t)(seed >> 32));
-  const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
-  const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);            // [0, 1)
-  const float u3 = ((float)(c[2] >> 8) + 1.0f) * (1.0f / 16777216.0f);
-  const float u4 = (float)(c[3] >> 8) * (1.0f / 16777216.0f);
-  const float r1 = sqrtf(-2.0f * logf(u1)), r2 = sqrtf(-2.0f * logf(u3));
-  float s1, c1, s2, c2;
-  sincospif(2.0f * u2, &s1, &c1);
-  sincospif(2.0f * u4, &s2, &c2);
-  z[0] = r1 * c1;
-  z[1] = r1 * s1;
-  z[2] = r2 * c2;
-  z[3] = r2 * s2;
-}
-
-// --------------------------------------------------------------------------
-// Euler-Maruyama rollout  (DeepBSDE.py:218-222, nd_BSPDE_case.py:258-261)
-// thread per (path m, dim d); sequential over n.  Writes the network input
-// rows xin[r] = [t, X_1..X_D, 1, 0...] and sdw[r] = sigma(X_n) * dW_n.
-// The arithmetic order and rounding is the reference's (no contraction):
-//   X1 = (X0 + (mu_a*X0)*(t1-t0)) + (sig_a*X0 + sig_b)*(W1-W0)
-// --------------------------------------------------------------------------
-struct RolloutArgs {
-  int M, N, D, ldx;
-  const float* t;   // [M, N+1] or null (uniform grid)
-  const float* W;   // [M, N+1, D] or null (Philox)
-  const float* Xi;  // [xi_rows, D]
-  int xi_rows;
-  float T;
-  unsigned long long seed, offset;
-  long long path0;
-  float mu_a, sig_a, sig_b;
-  float* xin;       // [Rp, ldx]
-  float* sdw;       // [Rp, ldx]   (cols 1..D, aligned with X in xin)
-};
-
-__global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
-  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= p.M * p.D) return;
-  const int m = gid / p.D, d = gid - m * p.D;
-  const int N1 = p.N + 1;
-  float x = p.Xi[(p.xi_rows == 1 ? 0 : m) * p.D + d];
-  const float dtu = p.T / (float)p.N;
-  const float sqdt = sqrtf(dtu);
-  float t0 = p.t ? p.t[(size_t)m * N1] : 0.0f;
-  float w0 = p.W ? p.W[(size_t)m * N1 * p.D + d] : 0.0f;
-  size_t r = (size_t)m * N1;
-  // blocks of 4 steps: the increments of a block (Philox, or the host W
-  // differences) are formed first, independent of x; then the sequential
-  // Euler-Maruyama updates
-  for (int n0 = 0; n0 < p.N; n0 += 4) {
-    float dw[4], t1[4];
-    if (p.W) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int n = min(n0 + k + 1, p.N);
-        const float w1 = p.W[((size_t)m * N1 + n) * p.D + d];
-        t1[k] = p.t[(size_t)m * N1 + n];
-        dw[k] = __fsub_rn(w1, w0);
-        w0 = w1;
-      }
-    } else {
-      float z[4];
-      philox_normal4(p.seed, p.offset, (uint32_t)(p.path0 + m), (uint32_t)(n0 >> 2), (uint32_t)d, z);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int n = min(n0 + k + 1, p.N);
-        t1[k] = p.t ? p.t[(size_t)m * N1 + n] : (float)((double)p.T * (double)n / (double)p.N);
-        dw[k] = sqdt * z[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (n0 + k >= p.N) break;
-      float* xr = p.xin + r * p.ldx;
-      xr[1 + d] = x;
-      if (d == 0) {
-        xr[0] = t0;
-        xr[p.D + 1] = 1.0f;
-      }
-      const float dt = __fsub_rn(t1[k], t0);
-      const float sg = __fadd_rn(__fmul_rn(p.sig_a, x), p.sig_b);
-      const float s = __fmul_rn(sg, dw[k]);
-      p.sdw[r * p.ldx + 1 + d] = s;
-      x = __fadd_rn(__fadd_rn(x, __fmul_rn(__fmul_rn(p.mu_a, x), dt)), s);
-      t0 = t1[k];
-      ++r;
-    }
-  }
-  float* xr = p.xin + r * p.ldx;  // n = N
-  xr[1 + d] = x;
-  p.sdw[r * p.ldx + 1 + d] = 0.0f;
-  if (d == 0) {
-    xr[0] = t0;
-    xr[p.D + 1] = 1.0f;
-  }
-}
-
-// Q3 (D == 1): S_n = sum over paths of sdw[m, n]   (1d_BSPDE_case.py:271-273)
-__global__ void __launch_bounds__(256) q3_sum_kernel(const float* sdw, int ldx, int M, int N, float* S) {
-  const int n = blockIdx.x;
-  __shared__ float red[256];
-  float acc = 0.f;
-  for (int m = threadIdx.x; m < M; m += 256) acc += sdw[((size_t)m * (N + 1) + n) * ldx + 1];
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) S[n] = red[0];
+__device__ __forceinline__ float terminal_dg(int kind, float x, float gsc) {
+  return kind == 0 ? 2.f * x : (kind == 3 ? x * gsc : gsc);
 }
 
 // --------------------------------------------------------------------------
@@ -283,8 +181,9 @@ struct ChainArgs {
   int ldx;
   const float* u;     // [Rp]
   const float* q3S;   // [N] or null
-  float phi_r, phi_c, phi_zz, strike;
-  int g_kind;
+  const float* umask; // [Rp] u-clamp gradient mask (heston_dnnpde.py:568) or null
+  float phi_r, phi_c, phi_zz, strike, g_alpha;
+  int g_kind, gcols;
   float* zbar;        // [Rp, ldx]
   float* rres;        // [Rp]
   float* lossrow;     // [Rp]
@@ -373,7 +272,7 @@ __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
   if constexpr (EPI == EPI_COTAN) {
     // Each 16-lane group owns 4 rows; the workgroup tile covers every column
     // (the engine launches this epilogue with a single column tile).
-    const int D = p.D;
+    const int D = p.D, G = p.gcols;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = rbase + j;
@@ -382,16 +281,23 @@ __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
       const bool term = n == p.N1 - 1;
       const float* xr = p.xin + (size_t)row * p.ldx;
       const float* sr = p.sdw + (size_t)row * p.ldx;
+      // Heston u clamp: Z = mask * grad u_raw, and the cotangents of the
+      // clamped u are masked the same way
+      const float um = p.umask ? p.umask[row] : 1.f;
       float s_zs = 0.f, s_xz = 0.f, s_zz = 0.f, s_x = 0.f, s_xx = 0.f, z1 = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int c = col0 + t * 16 + cl;  // Zfull column (0 = t, 1..D = Z)
-        const float z = acc[t][j];
+        const float z = acc[t][j] * um;
+        acc[t][j] = z;
         if (c >= 1 && c <= D) {
           const float xv = xr[c];
           s_zs += z * sr[c];
           s_xz += xv * z;
           s_zz += z * z;
+        }
+        if (c >= 1 && c <= G) {
+          const float xv = xr[c];
           s_x += xv;
           s_xx += xv * xv;
         }
@@ -417,22 +323,7 @@ __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
           lossv = res * res;
           coefY = -2.f * res;
         } else {
-          float g;
-          if (p.g_kind == 0) {
-            g = s_xx;
-          } else if (p.g_kind == 1) {
-            const float v = s_x - p.strike;
-            g = v > 0.f ? v : 0.f;
-            gsc = v > 0.f ? 1.f : 0.f;
-          } else if (p.g_kind == 2) {
-            const float v = s_x / (float)D - p.strike;
-            g = v > 0.f ? v : 0.f;
-            gsc = v > 0.f ? 1.f / (float)D : 0.f;
-          } else {
-            const float q = 0.5f + 0.5f * s_xx;
-            g = logf(q);
-            gsc = 1.f / q;
-          }
+          const float g = terminal_g(p.g_kind, s_x, s_xx, G, p.strike, p.g_alpha, gsc);
           res = y - g;
           lossv = res * res;
         }
@@ -449,12 +340,11 @@ __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
           if (!term) {
             const float dphidz = -p.phi_r * p.phi_c * xv + 2.f * p.phi_zz * z;
             const float sd = p.q3S ? S : sr[c];
-            zb = coefY * (dphidz * dt + sd);
-          } else {
-            const float dg = (p.g_kind == 0) ? 2.f * xv : (p.g_kind == 3 ? xv * gsc : gsc);
-            const float e = z - dg;
+            zb = um * (coefY * (dphidz * dt + sd));
+          } else if (c <= G) {
+            const float e = z - terminal_dg(p.g_kind, xv, gsc);
             tz += e * e;
-            zb = 2.f * e;
+            zb = um * (2.f * e);
           }
         }
         p.zbar[(size_t)row * p.ldx + c] = zb;
@@ -522,21 +412,29 @@ __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
 // u = h . w_out + b_out   (one 16-lane group per row)
 // --------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) rowdot_kernel(const float* H, int ldh, int ncols, const float* w,
-                                                     const float* b, float* u, int Rp) {
+                                                     const float* b, float* u, int Rp, float* umask) {
   const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
   const int cl = threadIdx.x & 15;
   if (row >= Rp) return;
   float s = 0.f;
   for (int c = cl; c < ncols; c += 16) s += H[(size_t)row * ldh + c] * w[c];
   s = red16(s);
-  if (cl == 0) u[row] = s + b[0];
+  if (cl == 0) {
+    const float v = s + b[0];
+    if (umask) {   // u = clamp(net, min=0) (heston_dnnpde.py:568); clamp passes the gradient at 0
+      umask[row] = v >= 0.f ? 1.f : 0.f;
+      u[row] = v >= 0.f ? v : 0.f;
+    } else {
+      u[row] = v;
+    }
+  }
 }
 
 // ubar[row] from the per-row residuals; loss partial sums per block.
 // rres[r] = Y_{n+1} - Ytilde_{n+1} (n < N), or Y_N - g(X_N) (n == N).
 __global__ void __launch_bounds__(256) ubar_kernel(const float* rres, const float* xin, int ldx, int R, int Rp,
                                                    int N1, float phi_r, const float* lossrow, float* ubar,
-                                                   float* u16, double* loss_part) {
+                                                   float* u16, double* loss_part, const float* umask) {
   const int row = blockIdx.x * 256 + threadIdx.x;
   float ub = 0.f;
   double lv = 0.0;
@@ -549,6 +447,7 @@ __global__ void __launch_bounds__(256) ubar_kernel(const float* rres, const floa
     } else {
       ub += 2.f * rres[row];
     }
+    if (umask) ub *= umask[row];
     lv = (double)lossrow[row];
   }
   if (row < Rp) {
@@ -744,17 +643,27 @@ __global__ void __launch_bounds__(256) sqnorm_kernel(const float* g, const unsig
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
+// optimizer kinds (include/dbsde.h DBSDE_OPT_*), each in torch.optim's
+// single-tensor formula order (the reference's CPU path; torch 2.10)
+enum OptKind { OPT_ADAM = 0, OPT_ADAMW, OPT_SGD, OPT_RMSPROP, OPT_ADAGRAD, OPT_ADAMAX, OPT_ADADELTA, OPT_ASGD };
+
 struct OptArgs {
   int kind;
   float lr, beta2, eps, wd, max_norm;
   float omb1, omb2;           // 1-beta1, 1-beta2 (computed in double, as torch's Python floats)
-  float step_size, bc2_sqrt;  // lr/(1-beta1^t), sqrt(1-beta2^t)
+  float step_size, bc2_sqrt;  // Adam: lr/(1-beta1^t), sqrt(1-beta2^t); Adamax/Adagrad: the step's clr
+  float alpha, rho;           // RMSprop alpha / Adadelta rho
+  float asgd_decay, asgd_eta; // ASGD: 1 - lambd*eta (double, cast), eta
+  int asgd_copy;              // ASGD: mu == 1 -> ax = p
+  float asgd_mu;
+  const float* loss;          // nullable: skip the whole update when the loss is not finite
   int nparts;
 };
 
 __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float* m, float* v, const unsigned char* used,
                                                     long long n, const double* part, OptArgs a) {
   __shared__ float clip_s;
+  __shared__ int skip_s;
   if (threadIdx.x == 0) {
     float coef = 1.f;
     if (a.max_norm > 0.f) {
@@ -765,28 +674,74 @@ __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float*
       if (coef > 1.f) coef = 1.f;
     }
     clip_s = coef;
+    skip_s = a.loss ? !isfinite(a.loss[0]) : 0;   // heston_dnnpde.py:409-411 NaN skip
   }
   __syncthreads();
+  if (skip_s) return;
   const float coef = clip_s;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     if (!used[i]) continue;
     float gi = g[i] * coef;
     g[i] = gi;
     float p = prm[i];
-    if (a.kind == 2) {  // SGD
-      if (a.wd != 0.f) gi = gi + a.wd * p;
-      prm[i] = p - a.lr * gi;
-      continue;
+    switch (a.kind) {
+      case OPT_SGD: {
+        if (a.wd != 0.f) gi = gi + a.wd * p;
+        prm[i] = p - a.lr * gi;
+        break;
+      }
+      case OPT_RMSPROP: {   // square_avg.mul_(alpha).addcmul_(g, g, 1-alpha); p.addcdiv_(g, sqrt(sa)+eps, -lr)
+        if (a.wd != 0.f) gi = gi + a.wd * p;
+        const float sa = v[i] * a.alpha + a.omb2 * gi * gi;
+        v[i] = sa;
+        prm[i] = p + (-a.lr) * (gi / (sqrtf(sa) + a.eps));
+        break;
+      }
+      case OPT_ADAGRAD: {   // state_sum.addcmul_(g, g, 1); p.addcdiv_(g, sqrt(ss)+eps, -clr)
+        if (a.wd != 0.f) gi = gi + a.wd * p;
+        const float ss = v[i] + gi * gi;
+        v[i] = ss;
+        prm[i] = p + (-a.step_size) * (gi / (sqrtf(ss) + a.eps));
+        break;
+      }
+      case OPT_ADAMAX: {    // exp_avg.lerp_(g, 1-b1); exp_inf = max(exp_inf*b2, |g|+eps); p.addcdiv_(m, u, -clr)
+        if (a.wd != 0.f) gi = gi + a.wd * p;
+        const float mi = m[i] + a.omb1 * (gi - m[i]);
+        const float ui = fmaxf(v[i] * a.beta2, fabsf(gi) + a.eps);
+        m[i] = mi;
+        v[i] = ui;
+        prm[i] = p + (-a.step_size) * (mi / ui);
+        break;
+      }
+      case OPT_ADADELTA: {  // sq.mul_(rho).addcmul_(g,g,1-rho); d = sqrt(acc+eps)/sqrt(sq+eps)*g; acc.mul_(rho).addcmul_(d,d,1-rho)
+        if (a.wd != 0.f) gi = gi + a.wd * p;
+        const float sq = v[i] * a.rho + a.omb2 * gi * gi;
+        const float dl = sqrtf(m[i] + a.eps) / sqrtf(sq + a.eps) * gi;
+        v[i] = sq;
+        m[i] = m[i] * a.rho + a.omb2 * dl * dl;
+        prm[i] = p + (-a.lr) * dl;
+        break;
+      }
+      case OPT_ASGD: {      // p.mul_(1 - lambd eta); p.add_(g, -eta); ax = p (mu == 1) or ax += (p - ax) mu
+        if (a.wd != 0.f) gi = gi + a.wd * p;
+        p = p * a.asgd_decay;
+        p = p + (-a.asgd_eta) * gi;
+        prm[i] = p;
+        m[i] = a.asgd_copy ? p : m[i] + (p - m[i]) * a.asgd_mu;
+        break;
+      }
+      default: {            // Adam / AdamW
+        if (a.kind == OPT_ADAMW) p = p * (1.f - a.lr * a.wd);   // decoupled decay
+        else if (a.wd != 0.f) gi = gi + a.wd * p;                // Adam L2
+        float mi = m[i];
+        mi = mi + a.omb1 * (gi - mi);                            // exp_avg.lerp_(g, 1-beta1)
+        float vi = v[i] * a.beta2 + a.omb2 * gi * gi;            // mul_(beta2).addcmul_(g, g, 1-beta2)
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
+        prm[i] = p - a.step_size * (mi / denom);                 // addcdiv_(m, denom, -step_size)
+      }
     }
-    if (a.kind == 1) p = p * (1.f - a.lr * a.wd);         // AdamW decoupled decay
-    else if (a.wd != 0.f) gi = gi + a.wd * p;             // Adam L2
-    float mi = m[i];
-    mi = mi + a.omb1 * (gi - mi);                         // exp_avg.lerp_(g, 1-beta1)
-    float vi = v[i] * a.beta2 + a.omb2 * gi * gi;         // mul_(beta2).addcmul_(g, g, 1-beta2)
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
-    prm[i] = p - a.step_size * (mi / denom);              // addcdiv_(m, denom, -step_size)
   }
 }
 

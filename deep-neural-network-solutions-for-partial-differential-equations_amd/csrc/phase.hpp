@@ -1,35 +1,42 @@
-// phase.hpp -- register-resident phase kernels (gfx950).
+// phase.hpp -- register-resident fused phase kernels (gfx950).
 //
-// The two network passes of the step, one wavefront per 16 rows:
-//   phaseA2 : forward (a_j, h_j, u) + input gradient (delta_j, g_j, Z) + the
-//             per-row sums the residual needs
-//   phaseC2 : forward tangent along zbar (adot_j, hdot_j) + reverse (p_j, alpha_j)
+// The two network passes of one deep-BSDE step, one wavefront per 16 rows
+// (= 16 (path, time) pairs), 4 waves (64 rows, one wave per SIMD) per
+// workgroup, two workgroups per CU:
+//   phaseA : forward (a_j, h_j, u) + input gradient (delta_j, g_j, Z) + the
+//            per-row sums the residual needs (net_u, DeepBSDE.py:189-194)
+//   phaseC : residuals and closed-form cotangents (ubar, zbar) of its rows,
+//            forward tangent along zbar (adot_j, hdot_j) + reverse (p_j,
+//            alpha_j) (loss.backward, DeepBSDE.py:279)
 //
 // Orientation.  Every layer is computed transposed, out^T = W . act^T: the
 // weights are the MFMA A operand and the activations the B operand, so with
 // v_mfma_f32_16x16x4_f32 lane l = cl + 16 q holds, for batch row cl, the
 // output columns 16 o + 4 q + r (r = 0..3) of every 16-column block o.  That is
-// exactly the B-operand layout the next layer needs (k-step (t, r) pairs
-// logical k = q with column 16 t + 4 q + r), so activations never leave the
-// registers between layers: no LDS re-layout, no per-layer barrier for
-// activations, float4 global loads/stores of whole 16-byte column groups.
+// exactly the B-operand layout the next layer needs, so activations never
+// leave the registers between layers (no LDS re-layout, no per-layer barrier
+// for activations, float4 global loads/stores of whole 16-byte column groups).
 //
 // Weights.  Each operand matrix is packed once per step (pack_tagged_kernel)
-// into a "fragment image": fragment (o, t) is 64 lanes x float4 with lane l
-// holding W[16 o + (l & 15)][16 t + 4 (l >> 4) .. + 3].  A workgroup of 8 waves
-// (128 rows, two waves per SIMD) streams the images of its stage sequence
-// through two LDS buffers with LDS-DMA (global_load_lds_dwordx4, one 1 KiB
-// fragment per wave-instruction, no VGPRs): while stage s computes out of one
-// buffer the image of stage s+1 lands in the other, and one barrier per stage
-// (not per K chunk) publishes it.  Fragment reads are lane-linear ds_read_b128
-// (conflict-free).
+// into a t-major "fragment image": fragment (o, t) = 64 lanes x float4, lane l
+// holding W[16 o + (l & 15)][16 t + 4 (l >> 4) .. + 3], at index t * TO + o.
+// Every image is streamed through LDS in two pieces, input blocks [0, H) and
+// [H, TI), H = ceil(TI / 2), double buffered with LDS-DMA
+// (global_load_lds_dwordx4, one 1 KiB fragment per wave instruction): two
+// workgroups fit in a CU (2 x 2 x 28 KB at TI = TO = 7).  Fragment reads are
+// lane-linear ds_read_b128 (conflict-free).
+//
+// Stores.  An activation tile that the next layer also consumes (h, hdot,
+// delta, g, alpha) is stored right after the next piece's barrier instead of
+// just before it, so the vmcnt(0) that retires a piece's LDS-DMA does not
+// wait on stores issued a few cycles earlier.
 #pragma once
 #include "fused.hpp"
 
 namespace dbsde {
 
-constexpr int PH_WAVES = 8;
-constexpr int PH_ROWS = 16 * PH_WAVES;  // rows per workgroup; Rp is padded to this
+constexpr int P3_WAVES = 4;
+constexpr int P3_ROWS = 16 * P3_WAVES;
 
 // B-operand-layout tile <-> row-major global matrix (float4 per 16-col block)
 template <int TT>
@@ -41,9 +48,6 @@ __device__ __forceinline__ void bload(Mat<TT>& m, const float* base, int ld, int
 }
 template <int TT>
 __device__ __forceinline__ void bstore(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
-#ifdef DBSDE_EXP_NOSTORE
-  if (base != nullptr) return;   // timing experiment only: activation stores dropped
-#endif
   const int lane = threadIdx.x & 63;
   float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);
 #pragma unroll
@@ -54,27 +58,21 @@ __device__ __forceinline__ void glds16(const float* g, floatx4* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
-// wave w copies fragments w, w + 8, ... of an nf-fragment image
-__device__ __forceinline__ void stage_dma(const float* img, int nf, floatx4* buf, int wave, int lane) {
-  for (int f = wave; f < nf; f += PH_WAVES) glds16(img + (size_t)f * 256 + lane * 4, buf + f * 64);
-}
 __device__ __forceinline__ void vm_wait0() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0)
 
-// acc[o] += W(o, :) . b  over TI input blocks; W from a fragment image in LDS
-// Output blocks are taken in groups of at most OG (fragment registers 4 OG;
-// OG >= 2 keeps consecutive MFMAs on independent accumulators).
-template <int TO, int TI, int OG = 4>
-__device__ __forceinline__ void sgemm(Mat<TO>& acc, const Mat<TI>& b, const floatx4* img, int lane) {
+// acc[o] += sum_{t in [T0, T1)} W(o, t) . b(t); img = the piece holding
+// fragment (o, t) at ((t - T0) * TO + o).  Output blocks in groups of OG
+// (OG >= 2 keeps consecutive MFMAs on independent accumulators).
+template <int TO, int TI, int T0, int T1, int OG = 4>
+__device__ __forceinline__ void sgemm_piece(Mat<TO>& acc, const Mat<TI>& b, const floatx4* img, int lane) {
 #pragma unroll
-  for (int t = 0; t < TI; ++t) {
+  for (int t = T0; t < T1; ++t) {
 #pragma unroll
     for (int o0 = 0; o0 < TO; o0 += OG) {
-      constexpr int dummy = 0;
-      (void)dummy;
       floatx4 w[OG];
 #pragma unroll
       for (int o = 0; o < OG; ++o)
-        if (o0 + o < TO) w[o] = img[((o0 + o) * TI + t) * 64 + lane];
+        if (o0 + o < TO) w[o] = img[((t - T0) * TO + o0 + o) * 64 + lane];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -84,8 +82,13 @@ __device__ __forceinline__ void sgemm(Mat<TO>& acc, const Mat<TI>& b, const floa
   }
 }
 
-// stage sequencer: wait for this stage's image, publish it, start the next one
-struct Stager {
+// wave w copies fragments w, w + 4, ... of an nf-fragment piece
+__device__ __forceinline__ void piece_dma(const float* img, int nf, floatx4* buf, int wave, int lane) {
+  for (int f = wave; f < nf; f += P3_WAVES) glds16(img + (size_t)f * 256 + lane * 4, buf + f * 64);
+}
+
+// piece sequencer: wait for this piece, publish it, start the next one
+struct PieceStager {
   floatx4* wl;
   const float* const* img;
   const int* nf;
@@ -93,74 +96,87 @@ struct Stager {
   __device__ __forceinline__ const floatx4* next() {
     vm_wait0();
     __syncthreads();
-    if (st + 1 < n) stage_dma(img[st + 1], nf[st + 1], wl + ((st + 1) & 1) * buf, wave, lane);
+    if (st + 1 < n) piece_dma(img[st + 1], nf[st + 1], wl + ((st + 1) & 1) * buf, wave, lane);
     const floatx4* cur = wl + (st & 1) * buf;
     ++st;
     return cur;
   }
 };
 
+struct NoOp {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// one stage = one operand image: two pieces (one when TI == 1); `after` runs
+// right after the first piece's barrier (deferred stores, early loads)
+template <int TO, int TI, class F>
+__device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceStager& sg, int lane, F&& after) {
+  constexpr int H = (TI + 1) / 2;
+  const floatx4* w = sg.next();
+  after();
+  sgemm_piece<TO, TI, 0, H>(acc, b, w, lane);
+  if constexpr (H < TI) {
+    w = sg.next();
+    sgemm_piece<TO, TI, H, TI>(acc, b, w, lane);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // phase A: forward + input gradient + Z (+ residual row sums)
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, {[Z_j], B_j} j=K..1, Z0
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT>
-__global__ void __launch_bounds__(512, 2) phaseA2_kernel(FusedArgs p) {
-  constexpr int TB = T > TD ? T : TD, BUF = TB * TB * 64;
+__global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
+  constexpr int TB = T > TD ? T : TD, BUF = ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[2 * BUF];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int row0 = blockIdx.x * PH_ROWS + wave * 16;
+  const int row0 = blockIdx.x * P3_ROWS + wave * 16;
   const int S = p.S, Wd = p.W;
-  Stager sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
-  stage_dma(p.simgA[0], p.snfA[0], wl, wave, lane);
+  PieceStager sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
+  piece_dma(p.simgA[0], p.snfA[0], wl, wave, lane);
   Mat<TD> x;
   bload(x, p.xin, p.Dp, row0, 0);
 
   Mat<T> s1[K + 1];   // act'(a_j)
   Mat<T> h, acc;
-  {  // level 0
-    const floatx4* w = sg.next();
+  zero(acc);
+  stage_mm<T, TD>(acc, x, sg, lane, NoOp{});
+  bstore(acc, p.Abuf, S, row0, 0);
+#pragma unroll
+  for (int o = 0; o < T; ++o)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float f, d;
+      act_v1<ACT>(acc.v[o][r], f, d);
+      h.v[o][r] = f;
+      s1[0].v[o][r] = d;
+    }
+  SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
     zero(acc);
-    sgemm<T, TD>(acc, x, w, lane);
+    stage_mm<T, T>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore(h, p.H, S, row0, (j - 1) * Wd); });
+    if (p.has_v) stage_mm<T, TD>(acc, x, sg, lane, NoOp{});
+#pragma unroll
+    for (int o = 0; o < T; ++o) {
+      const floatx4 bb = p.has_v ? floatx4{0.f, 0.f, 0.f, 0.f} : *(const floatx4*)(p.beta[j - 1] + 16 * o + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc.v[o][r] += bb[r];
+    }
+    bstore(acc, p.Abuf, S, row0, j * Wd);
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float f, d;
         act_v1<ACT>(acc.v[o][r], f, d);
-        h.v[o][r] = f;
-        s1[0].v[o][r] = d;
-      }
-    bstore(acc, p.Abuf, S, row0, 0);
-    bstore(h, p.H, S, row0, 0);
-  }
-  SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
-    constexpr int j = decltype(jc)::value;
-    const floatx4* w = sg.next();
-    zero(acc);
-    sgemm<T, T>(acc, h, w, lane);
-    if (p.has_v) {
-      w = sg.next();
-      sgemm<T, TD>(acc, x, w, lane);
-    }
-#pragma unroll
-    for (int o = 0; o < T; ++o) {
-      const floatx4 bb = p.has_v ? floatx4{0.f, 0.f, 0.f, 0.f} : *(const floatx4*)(p.beta[j - 1] + 16 * o + 4 * q);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float a = acc.v[o][r] + bb[r];
-        acc.v[o][r] = a;
-        float f, d;
-        act_v1<ACT>(a, f, d);
         s1[j].v[o][r] = d;
         h.v[o][r] = f + p.rho * h.v[o][r];
       }
-    }
-    bstore(acc, p.Abuf, S, row0, j * Wd);
-    bstore(h, p.H, S, row0, j * Wd);
   });
-  // u = h_{K+1} . w_out + b_out
+  // u = h_{K+1} . w_out + b_out  (clamped at 0 for Heston, heston_dnnpde.py:568;
+  // the clamp's gradient passes at u_raw >= 0, so Z = mask * grad u_raw)
+  float umask = 1.f;
   {
     float us = 0.f;
 #pragma unroll
@@ -171,8 +187,14 @@ __global__ void __launch_bounds__(512, 2) phaseA2_kernel(FusedArgs p) {
     }
     us += __shfl_xor(us, 16);
     us += __shfl_xor(us, 32);
-    if (q == 0) p.u[row0 + cl] = us + p.bout[0];
+    float uv = us + p.bout[0];
+    if (p.u_clamp) {
+      umask = uv >= 0.f ? 1.f : 0.f;
+      uv = uv >= 0.f ? uv : 0.f;
+    }
+    if (q == 0) p.u[row0 + cl] = uv;
   }
+  bstore(h, p.H, S, row0, K * Wd);
   // input gradient: g_{K+1} = w_out, delta_K = w_out act'(a_K)
   Mat<T> g, dl;
 #pragma unroll
@@ -184,20 +206,22 @@ __global__ void __launch_bounds__(512, 2) phaseA2_kernel(FusedArgs p) {
       dl.v[o][r] = wo[r] * s1[K].v[o][r];
     }
   }
-  bstore(dl, p.Delta, S, row0, K * Wd);
   Mat<TD> z;
   zero(z);
   SFor<0, K>::run([&](auto ic) __attribute__((always_inline)) {
     constexpr int j = K - decltype(ic)::value;
-    const floatx4* w;
-    if (p.has_v) {
-      w = sg.next();
-      sgemm<TD, T>(z, dl, w, lane);   // Z += delta_j V_j
-    }
-    w = sg.next();
+    auto prev = [&]() __attribute__((always_inline)) {   // (g_j, delta_j) of the previous step
+      if constexpr (j < K) bstore(g, p.G, S, row0, j * Wd);
+      bstore(dl, p.Delta, S, row0, j * Wd);
+    };
     Mat<T> gn;
     zero(gn);
-    sgemm<T, T>(gn, dl, w, lane);    // delta_j B_j
+    if (p.has_v) {
+      stage_mm<TD, T>(z, dl, sg, lane, prev);      // Z += delta_j V_j
+      stage_mm<T, T>(gn, dl, sg, lane, NoOp{});    // delta_j B_j
+    } else {
+      stage_mm<T, T>(gn, dl, sg, lane, prev);
+    }
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
@@ -206,19 +230,24 @@ __global__ void __launch_bounds__(512, 2) phaseA2_kernel(FusedArgs p) {
         g.v[o][r] = gv;
         dl.v[o][r] = gv * s1[j - 1].v[o][r];
       }
-    bstore(g, p.G, S, row0, (j - 1) * Wd);
-    bstore(dl, p.Delta, S, row0, (j - 1) * Wd);
   });
-  {
-    const floatx4* w = sg.next();
+  stage_mm<TD, T>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
+    bstore(g, p.G, S, row0, 0);
+    bstore(dl, p.Delta, S, row0, 0);
     bload(x, p.xin, p.Dp, row0, 0);
-    sgemm<TD, T>(z, dl, w, lane);    // Z += delta_0 W_in
+  });
+  if (p.u_clamp) {
+#pragma unroll
+    for (int o = 0; o < TD; ++o)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) z.v[o][r] *= umask;
   }
   bstore(z, p.zfull, p.Dp, row0, 0);
-  // residual row sums of row cl: [s_zs, s_xz, s_zz, s_x, s_xx, z1]
+  // residual row sums of row cl: [s_zs, s_xz, s_zz, s_x, s_xx, z1]; s_x, s_xx
+  // over the leading G state columns (the columns g reads)
   Mat<TD> sd;
   bload(sd, p.sdw, p.Dp, row0, 0);
-  const int D = p.D;
+  const int D = p.D, G = p.gcols;
   float s_zs = 0.f, s_xz = 0.f, s_zz = 0.f, s_x = 0.f, s_xx = 0.f, z1 = 0.f;
 #pragma unroll
   for (int o = 0; o < TD; ++o)
@@ -230,6 +259,8 @@ __global__ void __launch_bounds__(512, 2) phaseA2_kernel(FusedArgs p) {
         s_zs += zv * sd.v[o][r];
         s_xz += xv * zv;
         s_zz += zv * zv;
+      }
+      if (c >= 1 && c <= G) {
         s_x += xv;
         s_xx += xv * xv;
       }
@@ -243,95 +274,125 @@ __global__ void __launch_bounds__(512, 2) phaseA2_kernel(FusedArgs p) {
   }
   if (q == 0) {
     float* o = p.rowsum + (size_t)(row0 + cl) * 8;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) o[i] = v6[i];
+    *(floatx4*)o = floatx4{v6[0], v6[1], v6[2], v6[3]};
+    *(floatx4*)(o + 4) = floatx4{v6[4], v6[5], umask, 0.f};
   }
 }
 
 // ---------------------------------------------------------------------------
-// phase C: forward tangent along zbar + reverse over (primal, tangent)
+// phase C: cotangents + forward tangent along zbar + reverse over (primal, tangent)
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, B_j j=K..1
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT>
-__global__ void __launch_bounds__(512, 2) phaseC2_kernel(FusedArgs p) {
-  constexpr int TB = T > TD ? T : TD, BUF = TB * TB * 64;
+__global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
+  constexpr int TB = T > TD ? T : TD, BUF = ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[2 * BUF];
+  __shared__ double lsum[P3_WAVES];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int row0 = blockIdx.x * PH_ROWS + wave * 16;
+  const int row0 = blockIdx.x * P3_ROWS + wave * 16;
   const int S = p.S, Wd = p.W;
-  Stager sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
-  stage_dma(p.simgC[0], p.snfC[0], wl, wave, lane);
+  PieceStager sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
+  piece_dma(p.simgC[0], p.snfC[0], wl, wave, lane);
+
+  // ---- residuals and closed-form cotangents of row cl (every lane of the row
+  // computes them; the zbar columns 16 o + 4 q + r are this lane's)
+  const CotanParams& cp = p.cp;
+  const int r = row0 + cl;
+  const RowCotan rc = row_cotan(cp, r);
   Mat<TD> zb;
-  bload(zb, p.zbar, p.Dp, row0, 0);
+  float tz = 0.f;
+  {
+    const size_t off = (size_t)r * p.Dp + 4 * q;
+#pragma unroll
+    for (int o = 0; o < TD; ++o) {
+      const floatx4 xv = *(const floatx4*)(cp.xin + off + 16 * o);
+      const floatx4 zv = *(const floatx4*)(cp.zfull + off + 16 * o);
+      const floatx4 sv = *(const floatx4*)(cp.sdw + off + 16 * o);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int c = 16 * o + 4 * q + rr;
+        zb.v[o][rr] = (rc.valid && c >= 1 && c <= p.D) ? col_zbar(cp, rc, c, xv[rr], zv[rr], sv[rr], tz) : 0.f;
+      }
+    }
+  }
+  bstore(zb, p.zbar, p.Dp, row0, 0);
+  tz += __shfl_xor(tz, 16);
+  tz += __shfl_xor(tz, 32);
+  {
+    // loss of the workgroup's rows, fixed order: rows within the wave, then waves
+    double lv = (rc.valid && q == 0) ? (double)(rc.res * rc.res + tz) : 0.0;
+#pragma unroll
+    for (int s = 1; s < 16; s <<= 1) lv += __shfl_xor(lv, s);
+    if (lane == 0) lsum[wave] = lv;
+    if (q == 0) {
+      p.ubar[r] = rc.ub;
+      if (p.u16) p.u16[(size_t)r * 16] = rc.ub;
+    }
+  }
 
   Mat<T> ad[K + 1];   // adot_j
   Mat<T> hd, av;
-  {  // tangent level 0
-    const floatx4* w = sg.next();
+  zero(ad[0]);
+  stage_mm<T, TD>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
     bload(av, p.Abuf, S, row0, 0);
-    zero(ad[0]);
-    sgemm<T, TD>(ad[0], zb, w, lane);
+    if (threadIdx.x == 0) p.loss_part[blockIdx.x] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
+  });
 #pragma unroll
-    for (int o = 0; o < T; ++o)
+  for (int o = 0; o < T; ++o)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) hd.v[o][r] = act_1<ACT>(av.v[o][r]) * ad[0].v[o][r];
-    bstore(hd, p.Hdot, S, row0, 0);
-  }
+    for (int rr = 0; rr < 4; ++rr) hd.v[o][rr] = act_1<ACT>(av.v[o][rr]) * ad[0].v[o][rr];
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    const floatx4* w = sg.next();
-    bload(av, p.Abuf, S, row0, j * Wd);
     zero(ad[j]);
-    sgemm<T, T>(ad[j], hd, w, lane);
-    if (p.has_v) {
-      w = sg.next();
-      sgemm<T, TD>(ad[j], zb, w, lane);
-    }
+    stage_mm<T, T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
+      bstore(hd, p.Hdot, S, row0, (j - 1) * Wd);
+      bload(av, p.Abuf, S, row0, j * Wd);
+    });
+    if (p.has_v) stage_mm<T, TD>(ad[j], zb, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) hd.v[o][r] = act_1<ACT>(av.v[o][r]) * ad[j].v[o][r] + p.rho * hd.v[o][r];
-    bstore(hd, p.Hdot, S, row0, j * Wd);
+      for (int rr = 0; rr < 4; ++rr) hd.v[o][rr] = act_1<ACT>(av.v[o][rr]) * ad[j].v[o][rr] + p.rho * hd.v[o][rr];
   });
+  bstore(hd, p.Hdot, S, row0, K * Wd);
   // reverse: p_{K+1} = ubar w_out ; alpha_K = w_out (ubar act'(a_K) + adot_K act''(a_K))
   Mat<T> pv, al;
   {
-    const float ub = p.ubar[row0 + cl];
+    const float ub = rc.ub;
 #pragma unroll
     for (int o = 0; o < T; ++o) {
       const floatx4 wo = *(const floatx4*)(p.wout + 16 * o + 4 * q);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int rr = 0; rr < 4; ++rr) {
         float d1, d2;
-        act_12<ACT>(av.v[o][r], d1, d2);
-        pv.v[o][r] = ub * wo[r];
-        al.v[o][r] = wo[r] * (ub * d1 + ad[K].v[o][r] * d2);
+        act_12<ACT>(av.v[o][rr], d1, d2);
+        pv.v[o][rr] = ub * wo[rr];
+        al.v[o][rr] = wo[rr] * (ub * d1 + ad[K].v[o][rr] * d2);
       }
     }
-    bstore(al, p.Alpha, S, row0, K * Wd);
   }
   SFor<0, K>::run([&](auto ic) __attribute__((always_inline)) {
     constexpr int j = K - decltype(ic)::value;
-    const floatx4* w = sg.next();
-    bload(av, p.Abuf, S, row0, (j - 1) * Wd);
-    Mat<T> acc;
+    Mat<T> acc, gg;
     zero(acc);
-    sgemm<T, T>(acc, al, w, lane);   // alpha_j B_j
-    Mat<T> gg;
-    bload(gg, p.G, S, row0, (j - 1) * Wd);
+    stage_mm<T, T>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
+      bstore(al, p.Alpha, S, row0, j * Wd);
+      bload(av, p.Abuf, S, row0, (j - 1) * Wd);
+      bload(gg, p.G, S, row0, (j - 1) * Wd);
+    });
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pp = acc.v[o][r] + p.rho * pv.v[o][r];
-        pv.v[o][r] = pp;
+      for (int rr = 0; rr < 4; ++rr) {
+        const float pp = acc.v[o][rr] + p.rho * pv.v[o][rr];
+        pv.v[o][rr] = pp;
         float d1, d2;
-        act_12<ACT>(av.v[o][r], d1, d2);
-        al.v[o][r] = pp * d1 + gg.v[o][r] * ad[j - 1].v[o][r] * d2;
+        act_12<ACT>(av.v[o][rr], d1, d2);
+        al.v[o][rr] = pp * d1 + gg.v[o][rr] * ad[j - 1].v[o][rr] * d2;
       }
-    bstore(al, p.Alpha, S, row0, (j - 1) * Wd);
   });
+  bstore(al, p.Alpha, S, row0, 0);
 }
 
 }  // namespace dbsde

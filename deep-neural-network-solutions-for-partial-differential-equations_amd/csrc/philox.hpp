@@ -1,0 +1,48 @@
+// philox.hpp -- Philox4x32-10 counter-based generator and Box-Muller normals
+// (device side of the Brownian increments; restated in oracle/philox.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dbsde {
+
+// --------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11; Random123 constants) + Box-Muller
+// --------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]), lo0 = 0xD2511F53u * c[0];
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]), lo1 = 0xCD9E8D57u * c[2];
+    const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0;
+    c[1] = lo1;
+    c[2] = n2;
+    c[3] = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+
+// Four standard normals from one Philox block: both Box-Muller outputs of the
+// uniform pairs (c0, c1) and (c2, c3).  Counter (d, n/4, m, offset), key
+// (seed ^ offset_hi, seed_hi); z[k] is the draw of step 4 (n/4) + k.
+__device__ __forceinline__ void philox_normal4(unsigned long long seed, unsigned long long offset, uint32_t m,
+                                               uint32_t nq, uint32_t d, float z[4]) {
+  uint32_t c[4] = {d, nq, m, (uint32_t)offset};
+  philox4x32_10(c, (uint32_t)seed ^ (uint32_t)(offset >> 32), (uint32_t)(seed >> 32));
+  const float u1 = ((float)(c[0] >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
+  const float u2 = (float)(c[1] >> 8) * (1.0f / 16777216.0f);            // [0, 1)
+  const float u3 = ((float)(c[2] >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  const float u4 = (float)(c[3] >> 8) * (1.0f / 16777216.0f);
+  const float r1 = sqrtf(-2.0f * logf(u1)), r2 = sqrtf(-2.0f * logf(u3));
+  float s1, c1, s2, c2;
+  sincospif(2.0f * u2, &s1, &c1);
+  sincospif(2.0f * u4, &s2, &c2);
+  z[0] = r1 * c1;
+  z[1] = r1 * s1;
+  z[2] = r2 * c2;
+  z[3] = r2 * s2;
+}
+
+}  // namespace dbsde

@@ -13,7 +13,9 @@ rejected at construction.
 Multi-GPU: when torch.distributed is initialised (one process per GPU), the
 M paths of every minibatch are split into contiguous blocks of M/world per
 rank; gradients and loss are summed with one all-reduce per step and the
-optimizer runs replicated.
+optimizer runs replicated.  In parity mode every rank draws the
+same global numpy batch (the reference's stream) and uploads only its slice;
+in device mode the Philox stream is keyed by the global path index.
 """
 from __future__ import annotations
 
@@ -29,7 +31,19 @@ from . import networks
 from .solver import NativeSolver, ProblemSpec
 
 OPTIMIZER_NAMES = ("Adam", "SGD", "RMSprop", "AdamW", "Adadelta", "Adagrad", "Adamax", "ASGD", "LBFGS")
-NATIVE_OPTIMIZERS = ("Adam", "AdamW", "SGD")
+NATIVE_OPTIMIZERS = ("Adam", "SGD", "RMSprop", "AdamW", "Adadelta", "Adagrad", "Adamax", "ASGD")
+# torch.optim defaults of each optimizer as the reference builds it, optim.X(params, lr=lr)
+# (nd_BSPDE_case.py:331-350; torch 2.10 signatures)
+OPT_DEFAULTS = {
+    "Adam": dict(betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0),
+    "AdamW": dict(betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2),
+    "SGD": dict(weight_decay=0.0),
+    "RMSprop": dict(alpha=0.99, eps=1e-8, weight_decay=0.0),
+    "Adagrad": dict(eps=1e-10, lr_decay=0.0, weight_decay=0.0),
+    "Adamax": dict(betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0),
+    "Adadelta": dict(rho=0.9, eps=1e-6, weight_decay=0.0),
+    "ASGD": dict(lambd=1e-4, alpha=0.75, t0=1e6, weight_decay=0.0),
+}
 
 
 def _default_device():
@@ -50,16 +64,17 @@ class FBSNN(ABC):
     # reference behaviour switches (nd v2 defaults)
     clip_max_norm = 1.0          # nd_BSPDE_case.py:383 (DeepBSDE: none)
     schedule = "nd"              # Q1: "nd" (nd_BSPDE_case.py:364-368), "corr" (with_corr:406-409) or None
+    skip_nonfinite = False       # heston_dnnpde.py:409-411 skips an iteration whose loss is NaN
     log_every = 100
 
     def __init__(self, Xi, T, M, N, D, Mm, layers, mode, activation, correlation_type="no_correlation",
                  device=None):
         self.device = torch.device(device) if device is not None else _default_device()
-        self.Xi = torch.as_tensor(np.asarray(Xi), dtype=torch.float32).to(self.device)
         self.T, self.M, self.N, self.D, self.Mm = T, M, N, D, Mm
         self.strike = self._default_strike()
         self.mode, self.activation = mode, activation
-        self.layers = list(layers)
+        self.layers = self._native_layers(list(layers))
+        self.Xi = self._initial_state(Xi)
         spec = self.problem_spec()
         if not isinstance(spec, ProblemSpec):
             raise NotImplementedError(
@@ -67,7 +82,7 @@ class FBSNN(ABC):
                 "sigma_tf cannot run on the native path")
         self.spec = spec
         self.solver = NativeSolver(mode, self.layers, activation, spec, T, self.device)
-        self.model = networks.make_model(mode, self.layers, activation)
+        self.model = self._make_model(list(layers))
         self.params = networks.flatten_into(self.model, self.device)
         if self.params.numel() != self.solver.nparams:
             raise RuntimeError("native parameter layout does not match the module layout")
@@ -77,13 +92,24 @@ class FBSNN(ABC):
         self.training_loss = []
         self.iteration = []
         self.correlation_type = correlation_type
-        self.correlation_matrix = self.generate_correlation_matrix(D)
+        self.correlation_matrix = self.generate_correlation_matrix(self.solver.nb)
         self._L = None if correlation_type == "no_correlation" else np.linalg.cholesky(self.correlation_matrix)
+        if self._L is not None and spec.kind == "diag":
+            self.solver.set_corr(self._L)       # device mode: L staged in LDS by the path kernel
         self.rank, self.world = _world()
 
     # ------------------------------------------------------------------ problem
     def _default_strike(self):
         return 1.0 * self.D          # nd_BSPDE_case.py:147
+
+    def _native_layers(self, layers):
+        return layers
+
+    def _initial_state(self, Xi):
+        return torch.as_tensor(np.asarray(Xi), dtype=torch.float32).to(self.device)
+
+    def _make_model(self, layers):
+        return networks.make_model(self.mode, layers, self.activation)
 
     def problem_spec(self):
         return None
@@ -99,6 +125,10 @@ class FBSNN(ABC):
 
     def sigma_tf(self, t, X, Y):
         return torch.diag_embed(torch.ones([X.shape[0], self.D], device=X.device))
+
+    @property
+    def state_dim(self):
+        return self.layers[0] - 1
 
     # ------------------------------------------------------------------ correlation (with_corr:186-212)
     def generate_correlation_matrix(self, D):
@@ -127,40 +157,55 @@ class FBSNN(ABC):
         return c
 
     # ------------------------------------------------------------------ solver core
-    def fetch_minibatch(self):
-        """DeepBSDE.py:247-262 / with_corr:316-353: host numpy draws (the parity
-        stream), returned on the device."""
-        M, N, D, T = self.M, self.N, self.D, self.T
+    def _host_minibatch(self, M=None):
+        """DeepBSDE.py:247-262 / with_corr:316-353: the reference's numpy draw
+        (the parity stream) in float64, cast to float32."""
+        M = self.M if M is None else M
+        N, nb, T = self.N, self.solver.nb, self.T
         Dt = np.zeros((M, N + 1, 1))
-        DW = np.zeros((M, N + 1, D))
+        DW = np.zeros((M, N + 1, nb))
         dt = T / N
         Dt[:, 1:, :] = dt
-        dw = np.sqrt(dt) * np.random.normal(size=(M, N, D))
+        dw = np.sqrt(dt) * np.random.normal(size=(M, N, nb))
         DW[:, 1:, :] = dw if self._L is None else np.einsum('ij,mnj->mni', self._L, dw)
-        t = torch.from_numpy(np.cumsum(Dt, axis=1)).float().to(self.device)
-        W = torch.from_numpy(np.cumsum(DW, axis=1)).float().to(self.device)
-        return t, W
+        return np.cumsum(Dt, axis=1).astype(np.float32), np.cumsum(DW, axis=1).astype(np.float32)
+
+    def fetch_minibatch(self):
+        """Host numpy draws (the reference's stream), returned on the device."""
+        t, W = self._host_minibatch()
+        return torch.from_numpy(t).to(self.device), torch.from_numpy(W).to(self.device)
+
+    def fetch_minibatch_device(self, seed=0, offset=0):
+        """Device fetch_minibatch (Philox, correlated by L when set): t [M,N+1,1], W [M,N+1,nb]."""
+        t, W = self.solver.brownian(self.M, self.N, seed=seed, offset=offset)
+        return t.unsqueeze(-1), W
 
     def _xi_rows(self, Xi, M):
-        Xi = torch.as_tensor(Xi, dtype=torch.float32).to(self.device).reshape(-1, self.D).contiguous()
+        Xi = torch.as_tensor(Xi, dtype=torch.float32).to(self.device).reshape(-1, self.state_dim).contiguous()
         if Xi.shape[0] not in (1, M):
             raise ValueError(f"Xi has {Xi.shape[0]} rows; expected 1 or {M}")
         return Xi
 
+    def _local_xi(self, p0, ml, M):
+        xi = self._xi_rows(self.Xi, M)
+        return xi if xi.shape[0] == 1 else xi[p0:p0 + ml].contiguous()
+
     def _run(self, t, W, Xi, grad=None, want=("X", "Y"), loss=None):
         """One native loss(+grad) evaluation over the paths of t/W."""
         M, N1 = t.shape[0], t.shape[1]
-        N = N1 - 1
+        N, Ds, nb = N1 - 1, self.state_dim, self.solver.nb
         Xi = self._xi_rows(Xi, M)
         out = {"loss": torch.empty(1, device=self.device) if loss is None else loss}
         if "X" in want:
-            out["X"] = torch.empty((M, N1, self.D), device=self.device)
+            out["X"] = torch.empty((M, N1, Ds), device=self.device)
         if "Y" in want:
             out["Y"] = torch.empty((M, N1, 1), device=self.device)
         if "Z" in want:
-            out["Z"] = torch.empty((M, N1, self.D), device=self.device)
-        self.solver.loss_grad(self.params, M, N, Xi, t=t.reshape(M, N1).contiguous().float(),
-                              W=W.reshape(M, N1, self.D).contiguous().float(), grad=grad, loss=out["loss"],
+            out["Z"] = torch.empty((M, N1, Ds), device=self.device)
+        t = torch.as_tensor(t, dtype=torch.float32).to(self.device)
+        W = torch.as_tensor(W, dtype=torch.float32).to(self.device)
+        self.solver.loss_grad(self.params, M, N, Xi, t=t.reshape(M, N1).contiguous(),
+                              W=W.reshape(M, N1, nb).contiguous(), grad=grad, loss=out["loss"],
                               X=out.get("X"), Y=out.get("Y"), Z=out.get("Z"))
         return out
 
@@ -170,7 +215,7 @@ class FBSNN(ABC):
         if X.dim() == 1:
             X = X.unsqueeze(-1)
         t = torch.as_tensor(t, dtype=torch.float32).to(self.device).reshape(-1).contiguous()
-        X = X.reshape(-1, self.D).contiguous()
+        X = X.reshape(-1, self.state_dim).contiguous()
         u = torch.empty((X.shape[0], 1), device=self.device)
         du = torch.empty_like(X)
         self.solver.net_u(self.params, t, X, u, du)
@@ -206,53 +251,12 @@ class FBSNN(ABC):
             return 0, M
         if M % self.world:
             raise ValueError(f"M={M} is not divisible by the world size {self.world}")
+        if self.state_dim == 1 and self.spec.q3:
+            # the reference's D == 1 Y-tilde term sums sigma*dW over ALL
+            # M paths, which a path-sharded rank cannot see
+            raise ValueError("the D == 1 squeeze-broadcast problems (q3) cannot be sharded over ranks")
         m = M // self.world
         return self.rank * m, m
-
-    def train_step(self, t, W, opt_state, optimizer_type, learning_rate, want_state=False):
-        """fetch -> loss/grad -> all-reduce -> clip -> optimizer step, on the
-        local shard of the minibatch.  Returns the device loss (and X, Y)."""
-        p0, ml = self._local_slice(t.shape[0])
-        xi = self.Xi if self.Xi.reshape(-1, self.D).shape[0] == 1 else self.Xi.reshape(-1, self.D)[p0:p0 + ml]
-        out = self._run(t[p0:p0 + ml], W[p0:p0 + ml], xi, grad=self.grad,
-                        want=("X", "Y") if want_state else (), loss=self._gradbuf[-1:])
-        return self._reduce_and_update(opt_state, optimizer_type, learning_rate), out
-
-    def _reduce_and_update(self, opt_state, optimizer_type, learning_rate):
-        if self.world > 1:
-            dist.all_reduce(self._gradbuf)     # RCCL over xGMI: [grad | loss], ~0.37 MB
-        opt_state["step"] += 1
-        self.solver.optimizer_step(self.params, self.grad, opt_state["m"], opt_state["v"], kind=optimizer_type,
-                                   lr=learning_rate, max_norm=self.clip_max_norm or 0.0,
-                                   step=opt_state["step"])
-        return self._gradbuf[-1:]
-
-    def device_step(self, opt_state, learning_rate, seed, optimizer_type="Adam"):
-        """Throughput-mode iteration: Brownian increments drawn on the device
-        (Philox, keyed by global path index), loss+grad, all-reduce, clip +
-        optimizer.  No host synchronisation; returns the device loss."""
-        p0, ml = self._local_slice(self.M)
-        xi = self._xi_rows(self.Xi, 1)
-        self.solver.loss_grad(self.params, ml, self.N, xi, seed=seed, path0=p0, grad=self.grad,
-                              loss=self._gradbuf[-1:])
-        return self._reduce_and_update(opt_state, optimizer_type, learning_rate)
-
-    def train_device(self, N_Iter, learning_rate, seed=0, optimizer_type="Adam"):
-        """train() with device-generated Brownian increments (no numpy stream,
-        no per-iteration host sync except every log_every iterations)."""
-        self._check_optimizer(optimizer_type)
-        previous_it = self.iteration[-1] if self.iteration else 0
-        opt_state = self.new_optimizer_state()
-        losses = []
-        for it in range(previous_it, previous_it + N_Iter):
-            self._schedule_n(it)
-            losses.append(self.device_step(opt_state, learning_rate, seed=(seed << 20) + it,
-                                           optimizer_type=optimizer_type).clone())
-            if it % self.log_every == 0:
-                self.training_loss.append(float(torch.cat(losses).mean()))
-                losses = []
-                self.iteration.append(it)
-        return np.stack((self.iteration, self.training_loss))
 
     def _check_optimizer(self, optimizer_type):
         if optimizer_type not in OPTIMIZER_NAMES:
@@ -261,23 +265,106 @@ class FBSNN(ABC):
             raise NotImplementedError(f"optimizer {optimizer_type!r} has no native implementation yet "
                                       f"(available: {', '.join(NATIVE_OPTIMIZERS)})")
 
-    def new_optimizer_state(self):
-        return {"m": torch.zeros_like(self.params), "v": torch.zeros_like(self.params), "step": 0}
+    def new_optimizer_state(self, optimizer_type="Adam", learning_rate=None):
+        """A fresh optimizer (the reference builds one per train() call, Q11)."""
+        self._check_optimizer(optimizer_type)
+        st = {"kind": optimizer_type, "lr": learning_rate, "m": torch.zeros_like(self.params),
+              "v": torch.zeros_like(self.params), "step": 0}
+        if optimizer_type == "ASGD":      # torch keeps eta and mu as fp32 state tensors
+            st["eta"] = float(np.float32(learning_rate if learning_rate is not None else 0.0))
+            st["mu"] = 1.0
+        return st
+
+    def _update(self, opt, learning_rate=None, skip_loss=None):
+        """clip_grad_norm_ (not for LBFGS) + optimizer.step() on the device."""
+        kind = opt["kind"]
+        lr = opt["lr"] if learning_rate is None else learning_rate
+        if kind == "ASGD" and opt["step"] == 0 and opt["lr"] is None:
+            opt["eta"] = float(np.float32(lr))
+        kw = OPT_DEFAULTS[kind]
+        opt["step"] += 1
+        self.solver.optimizer_step(
+            self.params, self.grad, opt["m"], opt["v"], kind=kind, lr=lr, betas=kw.get("betas", (0.9, 0.999)),
+            eps=kw.get("eps", 1e-8), weight_decay=kw["weight_decay"], max_norm=self.clip_max_norm or 0.0,
+            step=opt["step"], alpha=kw.get("alpha", 0.99) if kind == "RMSprop" else 0.99, rho=kw.get("rho", 0.9),
+            lr_decay=kw.get("lr_decay", 0.0), lambd=kw.get("lambd", 1e-4), asgd_eta=opt.get("eta", 0.0),
+            asgd_mu=opt.get("mu", 1.0), skip_nonfinite_loss=skip_loss)
+        if kind == "ASGD":                # torch.optim.asgd: eta / mu of the next step
+            t = float(opt["step"])
+            opt["eta"] = float(np.float32(lr / ((1 + kw["lambd"] * lr * t) ** kw["alpha"])))
+            opt["mu"] = float(np.float32(1 / max(1, t - kw["t0"])))
+
+    def _reduce(self):
+        if self.world > 1:
+            dist.all_reduce(self._gradbuf)     # RCCL over xGMI: [grad | loss], ~0.37 MB
+        return self._gradbuf[-1:]
+
+    def train_step(self, t, W, opt_state, optimizer_type=None, learning_rate=None, want_state=False):
+        """loss/grad on the local shard of a global minibatch (t, W: host numpy
+        or device tensors of all M paths) -> all-reduce -> clip -> optimizer
+        step.  Returns (device loss, outputs of the local shard)."""
+        M = t.shape[0]
+        p0, ml = self._local_slice(M)
+        out = self._run(t[p0:p0 + ml], W[p0:p0 + ml], self._local_xi(p0, ml, M), grad=self.grad,
+                        want=("X", "Y") if want_state else (), loss=self._gradbuf[-1:])
+        loss = self._reduce()
+        self._update(opt_state, learning_rate, skip_loss=loss if self.skip_nonfinite else None)
+        return loss, out
+
+    def device_step(self, opt_state, learning_rate=None, seed=0, optimizer_type=None):
+        """Throughput-mode iteration: Brownian increments drawn on the device
+        (Philox keyed by global path index, correlated by L when set),
+        loss+grad, all-reduce, clip + optimizer.  No host synchronisation;
+        returns the device loss."""
+        if self._L is not None and self.spec.kind != "diag":
+            raise NotImplementedError("device-mode correlated increments are implemented for diagonal problems")
+        p0, ml = self._local_slice(self.M)
+        self.solver.loss_grad(self.params, ml, self.N, self._local_xi(p0, ml, self.M), seed=seed, path0=p0,
+                              grad=self.grad, loss=self._gradbuf[-1:])
+        loss = self._reduce()
+        self._update(opt_state, learning_rate, skip_loss=loss if self.skip_nonfinite else None)
+        return loss
+
+    def train_device(self, N_Iter, learning_rate, seed=0, optimizer_type="Adam"):
+        """train() with device-generated Brownian increments (no numpy stream,
+        no per-iteration host sync except every log_every iterations)."""
+        previous_it = self.iteration[-1] if self.iteration else 0
+        opt_state = self.new_optimizer_state(optimizer_type, learning_rate)
+        losses = []
+        for it in range(previous_it, previous_it + N_Iter):
+            self._schedule_n(it)
+            losses.append(self.device_step(opt_state, learning_rate, seed=(seed << 20) + it).clone())
+            if it % self.log_every == 0:
+                self.training_loss.append(float(torch.cat(losses).mean()))
+                losses = []
+                self.iteration.append(it)
+        return np.stack((self.iteration, self.training_loss))
+
+    def _record_y0(self, out):
+        pass
+
+    def _train_graph(self):
+        return np.stack((self.iteration, self.training_loss))
 
     def train(self, N_Iter, learning_rate, optimizer_type='Adam'):
         """nd_BSPDE_case.py:316-410 -> (graph, min_loss, min_loss_state)."""
-        self._check_optimizer(optimizer_type)
+        opt_state = self.new_optimizer_state(optimizer_type, learning_rate)   # fresh per call (Q11)
         loss_temp = []
         previous_it = self.iteration[-1] if self.iteration else 0
-        opt_state = self.new_optimizer_state()    # a fresh optimizer per call (Q11)
         start_time = time.time()
         min_loss, min_loss_state = float('inf'), None
         for it in range(previous_it, previous_it + N_Iter):
             self._schedule_n(it)
-            t_batch, W_batch = self.fetch_minibatch()
-            loss_t, out = self.train_step(t_batch, W_batch, opt_state, optimizer_type, learning_rate,
-                                          want_state=True)
-            loss = float(loss_t.item())
+            t_np, W_np = self._host_minibatch()       # the global batch; each rank uploads its slice
+            M = t_np.shape[0]
+            p0, ml = self._local_slice(M)
+            out = self._run(t_np[p0:p0 + ml], W_np[p0:p0 + ml], self._local_xi(p0, ml, M), grad=self.grad,
+                            want=("X", "Y"), loss=self._gradbuf[-1:])
+            loss = float(self._reduce().item())
+            if self.skip_nonfinite and not np.isfinite(loss):
+                print(f"NaN loss detected at iteration {it}. Skipping this iteration")
+                continue
+            self._update(opt_state, learning_rate)
             loss_temp.append(loss)
             if loss < min_loss:
                 min_loss = loss
@@ -292,14 +379,14 @@ class FBSNN(ABC):
                 self.training_loss.append(float(np.mean(loss_temp)))
                 loss_temp = []
                 self.iteration.append(it)
-        graph = np.stack((self.iteration, self.training_loss))
-        return graph, min_loss, min_loss_state
+                self._record_y0(out)
+        return self._train_graph(), min_loss, min_loss_state
 
     # ------------------------------------------------------------------ inference
     def predict(self, Xi_star, t_star, W_star):
         """nd_BSPDE_case.py:412-443 (sets self.M to the batch size)."""
         Xi_star = torch.as_tensor(np.asarray(Xi_star) if not isinstance(Xi_star, torch.Tensor) else Xi_star,
-                                  dtype=torch.float32).to(self.device).reshape(-1, self.D)
+                                  dtype=torch.float32).to(self.device).reshape(-1, self.state_dim)
         t_star = torch.as_tensor(t_star, dtype=torch.float32).to(self.device)
         W_star = torch.as_tensor(W_star, dtype=torch.float32).to(self.device)
         bs = max(Xi_star.shape[0], t_star.shape[0], W_star.shape[0])
@@ -317,10 +404,43 @@ class FBSNN(ABC):
                     'iteration': self.iteration}, file_name)
 
     def load_model(self, file_name):
-        ck = torch.load(file_name, map_location=self.device, weights_only=True)
+        """nd_BSPDE_case.py:452-456.  The reference stores training_loss as numpy
+        float64 scalars; they are allow-listed for the weights-only loader (no
+        arbitrary unpickling) and converted to Python floats."""
+        safe = [np.dtype, type(np.dtype(np.float64)), type(np.dtype(np.int64))]
+        try:
+            safe.append(np._core.multiarray.scalar)
+        except AttributeError:  # numpy < 2
+            safe.append(np.core.multiarray.scalar)
+        with torch.serialization.safe_globals(safe):
+            ck = torch.load(file_name, map_location=self.device, weights_only=True)
         self.model.load_state_dict(ck['model_state_dict'])
-        self.training_loss = list(ck['training_loss'])
-        self.iteration = list(ck['iteration'])
+        self.training_loss = [float(v) for v in ck['training_loss']]
+        self.iteration = [int(v) for v in ck['iteration']]
 
 
-__all__ = ["FBSNN", "ProblemSpec", "OPTIMIZER_NAMES", "NATIVE_OPTIMIZERS"]
+class PredictionGenerator:
+    """nd_BSPDE_case.py:543-584: num_samples batches of predictions from the
+    reference's numpy stream seeded with 42, concatenated over paths."""
+
+    def __init__(self, model, Xi, num_samples):
+        self.model = model
+        self.Xi = Xi
+        self.num_samples = num_samples
+
+    def generate_predictions(self):
+        np.random.seed(42)
+        ts, Xs, Ys = [], [], []
+        W_test = None
+        for _ in range(self.num_samples):
+            t_i, W_i = self.model.fetch_minibatch()
+            X_i, Y_i = self.model.predict(self.Xi, t_i, W_i)[:2]
+            if W_test is None:
+                W_test = W_i
+            ts.append(t_i.cpu().numpy())
+            Xs.append(X_i.cpu().numpy())
+            Ys.append(Y_i.cpu().numpy())
+        return np.concatenate(ts, 0), W_test, np.concatenate(Xs, 0), np.concatenate(Ys, 0)
+
+
+__all__ = ["FBSNN", "PredictionGenerator", "ProblemSpec", "OPTIMIZER_NAMES", "NATIVE_OPTIMIZERS", "OPT_DEFAULTS"]

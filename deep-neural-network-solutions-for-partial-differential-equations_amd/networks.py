@@ -112,6 +112,32 @@ def make_model(mode, layers, activation):
     return model
 
 
+def make_heston_model(mode, layers, activation, n_in):
+    """heston_dnnpde.py:519-585: the base FBSNN builds the network on the
+    reference's `layers` (input D + 1) with the usual init, HestonFBSNN then
+    replaces every input-facing Linear by one with n_in = 1 + 2k inputs
+    (t, S_1..S_k, v_1..v_k) and re-initialises all parameters (xavier_uniform_
+    gain 0.5 on matrices, zeros on vectors), in that RNG order."""
+    model = make_model(mode, layers, activation)
+    if mode == "FC":
+        model[0] = nn.Linear(n_in, layers[1])
+    elif mode == "Naisnet":
+        model.layer1 = nn.Linear(n_in, layers[1])
+        model.layer2_input = nn.Linear(n_in, layers[2])
+        if len(layers) >= 5:
+            model.layer3_input = nn.Linear(n_in, layers[3])
+        if len(layers) == 6:
+            model.layer4_input = nn.Linear(n_in, layers[4])
+    else:
+        raise ValueError("HestonFBSNN supports the 'FC' and 'Naisnet' modes (heston_dnnpde.py:156-167)")
+    for prm in model.parameters():
+        if prm.dim() > 1:
+            torch.nn.init.xavier_uniform_(prm, gain=0.5)
+        else:
+            torch.nn.init.zeros_(prm)
+    return model
+
+
 def flatten_into(model, device):
     """Copy the model's state into one flat fp32 device vector and rebind every
     parameter as a view of it.  Returns the flat vector."""

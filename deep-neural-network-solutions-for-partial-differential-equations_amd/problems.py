@@ -8,14 +8,17 @@ call them).
   BasketCallOption      with_corr...py:546-596          mean-payoff basket, correlated dW
   BSPDETestCase         with_corr...py:599-616          sum X^2 payoff, mu = 0.05 X
   HamiltonJacobiBellman hjb_implement.py:590-604        phi = |Z|^2, g = log(1/2 + |X|^2/2)
+  HestonFBSNN           heston_dnnpde.py:519-699        k-asset stochastic volatility
   BlackScholesBarenblatt: see deepbsde.py (DeepBSDE.py:326-341 surface)
 """
 from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 
+from . import networks
 from .fbsnn import FBSNN
 from .solver import ProblemSpec
 
@@ -131,4 +134,96 @@ class HamiltonJacobiBellman(FBSNN):
         return math.sqrt(2.0) * super().sigma_tf(t, X, Y)
 
 
-__all__ = ["CallOption", "CallOption1D", "BasketCallOption", "BSPDETestCase", "HamiltonJacobiBellman"]
+class HestonFBSNN(FBSNN):
+    """heston_dnnpde.py:519-699, generalised from one asset to k = D assets.
+
+    State [S_1..S_k, v_1..v_k] (k = 1 is the reference's [S, v]); one Brownian
+    motion per asset drives both S_i and v_i (the reference's FBSNN dimension is
+    1 and its einsum broadcasts dW, :522, :638); mu and the 2x2 diffusion block
+    of each asset are clamped to [-100, 100] (:591, :605); u = max(net, 0)
+    (:568); phi = 0.05 Y; the terminal payoff is the call on mean S (the
+    reference's max(S - 1, 0) at k = 1, or its sigmoid-smoothed "continuous"
+    variant, :546-558) and the terminal Z term uses dU/dS only (:654).  The
+    network takes (t, S, v) -- 1 + 2k inputs -- and is initialised as the
+    reference re-initialises it (xavier gain 0.5, zero biases, :580-585).
+    An iteration whose loss is NaN is skipped (:409-411).  k > 1 has no
+    reference golden; k = 1 is pinned by tests/golden/g1_heston_*."""
+
+    skip_nonfinite = True
+
+    def __init__(self, Xi, T, M, N, D, Mm, layers, mode, activation, correlation_type="no_correlation",
+                 kappa=2.0, theta=0.2, sigma=0.3, rho=0.8, v0=0.2, payoff_type='discontinuous', device=None):
+        if payoff_type not in ("discontinuous", "continuous"):
+            raise ValueError("Invalid payoff type. Choose 'discontinuous' or 'continuous'.")
+        self.kappa, self.theta, self.sigma, self.rho, self.v0 = kappa, theta, sigma, rho, v0
+        self.payoff_type = payoff_type
+        self.n_assets = D
+        self.Y0_values = []
+        self.y0_values = []
+        super().__init__(Xi, T, M, N, D, Mm, layers, mode, activation, correlation_type, device=device)
+
+    def _default_strike(self):
+        return 1.0
+
+    def _native_layers(self, layers):
+        return [1 + 2 * self.n_assets] + layers[1:]
+
+    def _make_model(self, layers):
+        return networks.make_heston_model(self.mode, layers, self.activation, 1 + 2 * self.n_assets)
+
+    def _full_state(self, Xi):
+        """[S_1..S_k] (or the reference's [S]) -> [S_1..S_k, v0..v0]."""
+        k = self.n_assets
+        x = torch.as_tensor(np.asarray(Xi) if not isinstance(Xi, torch.Tensor) else Xi,
+                            dtype=torch.float32).to(self.device)
+        x = x.reshape(-1, x.shape[-1]) if x.dim() > 1 else x.reshape(1, -1)
+        if x.shape[1] == 2 * k:
+            return x.contiguous()
+        S = x[:, :k]
+        return torch.cat([S, torch.full_like(S, self.v0)], 1).contiguous()
+
+    def _initial_state(self, Xi):
+        return self._full_state(Xi)
+
+    def problem_spec(self):
+        smooth = self.payoff_type == "continuous"
+        return ProblemSpec(kind="heston", mu_a=0.05, phi_r=0.05, phi_c=0.0, g="smooth_call" if smooth else "call_mean",
+                           strike=self.strike, g_alpha=10.0, g_cols=self.n_assets, u_clamp=True, q3=False,
+                           kappa=self.kappa, theta=self.theta, sigma=self.sigma, rho=self.rho)
+
+    def g_tf(self, X):
+        S = X[:, :self.n_assets] if X.dim() > 1 else X
+        a = torch.mean(S, dim=1, keepdim=True) - self.strike if S.dim() > 1 else S - self.strike
+        if self.payoff_type == "discontinuous":
+            return torch.maximum(a, torch.tensor(0.0, device=X.device))
+        return a / (1 + torch.exp(-10.0 * a))
+
+    def phi_tf(self, t, X, Y, Z):
+        return 0.05 * Y
+
+    def mu_tf(self, t, X, Y=None, Z=None):
+        k = self.n_assets
+        S, v = X[:, :k], X[:, k:]
+        return torch.cat([0.05 * S, self.kappa * (self.theta - v)], dim=1).clamp(-100, 100)
+
+    def _record_y0(self, out):
+        y0 = float(out["Y"][0, 0, 0])
+        self.Y0_values.append(y0)
+
+    def _train_graph(self):
+        return np.column_stack((self.iteration, self.training_loss, self.Y0_values))
+
+    def train(self, N_Iter, learning_rate, optimizer_type='Adam'):
+        """heston_dnnpde.py:345-450 -> graph [iteration, training_loss, Y0]."""
+        graph, _, _ = super().train(N_Iter, learning_rate, optimizer_type)
+        return graph
+
+    def predict(self, Xi_star, t_star, W_star):
+        """heston_dnnpde.py:661-683 -> (S, v, Y)."""
+        X, Y = super().predict(self._full_state(Xi_star), t_star, W_star)
+        k = self.n_assets
+        return X[:, :, :k], X[:, :, k:], Y
+
+
+__all__ = ["CallOption", "CallOption1D", "BasketCallOption", "BSPDETestCase", "HamiltonJacobiBellman",
+           "HestonFBSNN"]

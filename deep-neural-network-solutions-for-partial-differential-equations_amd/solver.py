@@ -17,8 +17,12 @@ from . import _lib
 @dataclass(frozen=True)
 class ProblemSpec:
     """Coefficients of one reference FBSNN subclass (see include/dbsde.h):
-    mu = mu_a X, sigma = diag(sig_a X + sig_b), phi = phi_r (Y - phi_c X.Z) + phi_zz |Z|^2,
-    g = g_kind(strike).  q3: reproduce the D == 1 squeeze broadcast."""
+    kind "diag":   mu = mu_a X, sigma = diag(sig_a X + sig_b)
+    kind "heston": k-asset Heston (heston_dnnpde.py:587-605) with S-drift mu_a,
+                   kappa/theta/sigma/rho, state [S_1..S_k, v_1..v_k]
+    phi = phi_r (Y - phi_c X.Z) + phi_zz |Z|^2, g = g_kind(strike, alpha) over
+    the first g_cols state columns (0 = all), u_clamp: u = max(net, 0).
+    q3: reproduce the D == 1 squeeze broadcast."""
 
     mu_a: float = 0.0
     sig_a: float = 0.0
@@ -29,12 +33,24 @@ class ProblemSpec:
     g: str = "sumsq"
     strike: float = 0.0
     q3: bool = True
+    kind: str = "diag"
+    g_cols: int = 0
+    g_alpha: float = 0.0
+    u_clamp: bool = False
+    kappa: float = 0.0
+    theta: float = 0.0
+    sigma: float = 0.0
+    rho: float = 0.0
 
     def to_c(self):
         if self.g not in _lib.G_KINDS:
             raise ValueError(f"unknown terminal condition {self.g!r}")
-        return _lib.Problem(self.mu_a, self.sig_a, self.sig_b, self.phi_r, self.phi_c, self.phi_zz,
-                            _lib.G_KINDS[self.g], self.strike, int(self.q3))
+        if self.kind not in _lib.PROBLEM_KINDS:
+            raise ValueError(f"unknown problem kind {self.kind!r}")
+        return _lib.Problem(_lib.PROBLEM_KINDS[self.kind], self.mu_a, self.sig_a, self.sig_b, self.phi_r,
+                            self.phi_c, self.phi_zz, _lib.G_KINDS[self.g], self.strike, int(self.q3),
+                            int(self.g_cols), self.g_alpha, int(self.u_clamp), self.kappa, self.theta,
+                            self.sigma, self.rho)
 
 
 def _ptr(t):
@@ -73,6 +89,7 @@ class NativeSolver:
         mask = (ctypes.c_ubyte * self.nparams)()
         _lib.check(self.lib.dbsde_param_used_mask(ctx, mask, self.nparams), ctx)
         self.used_mask = torch.frombuffer(bytearray(mask), dtype=torch.uint8).bool()
+        self.nb = int(self.lib.dbsde_brownian_dim(ctx))
 
     def __del__(self):
         ctx = getattr(self, "ctx", None)
@@ -130,16 +147,46 @@ class NativeSolver:
                    self.ctx)
 
     def optimizer_step(self, params, grad, m, v, kind="Adam", lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                       weight_decay=0.0, max_norm=0.0, step=1):
+                       weight_decay=0.0, max_norm=0.0, step=1, alpha=0.99, rho=0.9, lr_decay=0.0, lambd=1e-4,
+                       asgd_eta=0.0, asgd_mu=1.0, skip_nonfinite_loss=None):
+        """clip_grad_norm_ + optimizer.step() over the flat parameters; m, v are
+        the optimizer's state buffers (see include/dbsde.h DBSDE_OPT_*)."""
         if kind not in _lib.OPTIMIZERS:
             raise ValueError(f"Optimizer type '{kind}' is not recognized.")
         for name, v_ in (("params", params), ("grad", grad), ("m", m), ("v", v)):
             self._check_tensor(v_, name, self.nparams)
+        self._check_tensor(skip_nonfinite_loss, "loss", 1)
         o = _lib.Optim(_lib.OPTIMIZERS[kind], lr, betas[0], betas[1], eps, weight_decay,
-                       max_norm if max_norm else 0.0, int(step))
+                       max_norm if max_norm else 0.0, int(step), alpha, rho, lr_decay, lambd, asgd_eta, asgd_mu,
+                       _ptr(skip_nonfinite_loss))
         self._bind_stream()
         _lib.check(self.lib.dbsde_optimizer_step(self.ctx, _ptr(params), _ptr(grad), _ptr(m), _ptr(v),
                                                  ctypes.byref(o)), self.ctx)
+
+    # ------------------------------------------------------------------ Brownian increments
+    def set_corr(self, L):
+        """Cholesky factor for the device mode (None clears), with_corr...py:339-341."""
+        if L is None:
+            _lib.check(self.lib.dbsde_set_corr(self.ctx, None, 0), self.ctx)
+            return
+        import numpy as np
+        L = np.ascontiguousarray(np.asarray(L, dtype=np.float32))
+        if L.shape != (self.nb, self.nb):
+            raise ValueError(f"L must be [{self.nb}, {self.nb}]")
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_set_corr(self.ctx, L.ctypes.data_as(ctypes.c_void_p), self.nb), self.ctx)
+
+    def brownian(self, M, N, seed=0, offset=0, path0=0, increments=False):
+        """Device fetch_minibatch: (t [M, N+1], W [M, N+1, nb]) or, with
+        increments=True, (t, dW [M, N, nb]) as the device-mode rollout draws them."""
+        t = torch.empty((M, N + 1), device=self.device)
+        W = torch.empty((M, N if increments else N + 1, self.nb), device=self.device)
+        xi = torch.zeros(self.D, device=self.device)
+        b = _lib.Batch(int(M), int(N), None, None, int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1),
+                       int(path0), _ptr(xi), 1)
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_brownian(self.ctx, ctypes.byref(b), _ptr(t), _ptr(W), int(increments)), self.ctx)
+        return t, W
 
     # ------------------------------------------------------------------ profiling
     def profile(self, enable=True):
@@ -160,3 +207,43 @@ class NativeSolver:
                                                    ctypes.byref(by), ctypes.byref(nl)), self.ctx)
             out[name.value.decode()] = dict(ms=ms.value, flops=fl.value, bytes=by.value, launches=nl.value)
         return out
+
+
+# ---------------------------------------------------------------------- evaluators
+def exact(kind, t, X, T, params):
+    """Device exact / comparator solutions (include/dbsde.h dbsde_exact):
+    kind in {"bsb", "bs_call", "basket_avg", "basket_mean"}; t [R], X [R, D]
+    float32 cuda tensors.  Returns (price, delta); delta is None for "bsb"."""
+    lib = _lib.load()
+    if kind not in _lib.EXACT_KINDS:
+        raise ValueError(f"unknown exact solution {kind!r}")
+    X = X.reshape(X.shape[0], -1).contiguous().float()
+    t = t.reshape(-1).contiguous().float()
+    R, D = X.shape
+    if t.numel() != R or X.device.type != "cuda" or t.device != X.device:
+        raise ValueError("t [R] and X [R, D] must be float32 tensors on the same HIP device")
+    ncol = D if kind == "bs_call" else 1
+    price = torch.empty((R, ncol), device=X.device)
+    delta = None if kind == "bsb" else torch.empty((R, ncol), device=X.device)
+    import numpy as np
+    p = np.zeros(3, dtype=np.float64)
+    p[:len(params)] = params
+    s = torch.cuda.current_stream(X.device).cuda_stream
+    _lib.check(lib.dbsde_exact(_lib.EXACT_KINDS[kind], _ptr(t), _ptr(X), R, D, float(T),
+                               p.ctypes.data_as(ctypes.c_void_p), _ptr(price), _ptr(delta), ctypes.c_void_p(s)))
+    return price, delta
+
+
+def hjb_mc(t, X, T, mc=10 ** 5, seed=0):
+    """HJB Monte-Carlo value (hjb_implement.py:1088-1095) at P points."""
+    lib = _lib.load()
+    X = X.reshape(X.shape[0], -1).contiguous().float()
+    t = t.reshape(-1).contiguous().float()
+    P, D = X.shape
+    if t.numel() != P or X.device.type != "cuda" or t.device != X.device:
+        raise ValueError("t [P] and X [P, D] must be float32 tensors on the same HIP device")
+    u = torch.empty((P, 1), device=X.device)
+    s = torch.cuda.current_stream(X.device).cuda_stream
+    _lib.check(lib.dbsde_hjb_mc(_ptr(t), _ptr(X), P, D, float(T), int(mc), int(seed) & (2 ** 64 - 1), _ptr(u),
+                                ctypes.c_void_p(s)))
+    return u

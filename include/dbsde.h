@@ -2,9 +2,10 @@
  * dbsde.h -- C ABI of the MI355X-native deep-BSDE training step.
  *
  * This is the drop-in boundary for the reference's FBSNN solver surface
- * (nd_BSPDE_case.py:126-500, DeepBSDE.py:140-323).  Every entry point below
- * replaces one reference method; the Python binding that a maintainer adds
- * to a reference-style script is the ctypes class in
+ * (nd_BSPDE_case.py:126-500, DeepBSDE.py:140-323, with_corr...py:132-540,
+ * heston_dnnpde.py:519-699).  Every entry point below replaces one reference
+ * method; the Python binding that a maintainer adds to a reference-style script
+ * is the ctypes class in
  * deep-neural-network-solutions-for-partial-differential-equations_amd/fbsnn.py
  * (see INTEGRATION.md).
  *
@@ -30,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSDE_ABI_VERSION 1
+#define DBSDE_ABI_VERSION 2
 
 /* error codes */
 #define DBSDE_OK 0
@@ -49,28 +50,50 @@ extern "C" {
 #define DBSDE_ACT_RELU 1
 #define DBSDE_ACT_TANH 2
 
-/* terminal conditions g(X) */
-#define DBSDE_G_SUMSQ 0      /* sum X^2                 DeepBSDE.py:333-335          */
-#define DBSDE_G_CALL_SUM 1   /* max(sum X - K, 0)       nd_BSPDE_case.py:521-522     */
-#define DBSDE_G_CALL_MEAN 2  /* max(mean X - K, 0)      with_corr...py:577-579       */
-#define DBSDE_G_LOG 3        /* log(1/2 + 1/2 sum X^2)  hjb_implement.py:597-598     */
+/* terminal conditions g(X) over the leading g_cols state columns */
+#define DBSDE_G_SUMSQ 0       /* sum X^2                 DeepBSDE.py:333-335          */
+#define DBSDE_G_CALL_SUM 1    /* max(sum X - K, 0)       nd_BSPDE_case.py:521-522     */
+#define DBSDE_G_CALL_MEAN 2   /* max(mean X - K, 0)      with_corr...py:577-579,
+                                                         heston_dnnpde.py:550 (k = 1)  */
+#define DBSDE_G_LOG 3         /* log(1/2 + 1/2 sum X^2)  hjb_implement.py:597-598     */
+#define DBSDE_G_SMOOTH_CALL 4 /* a / (1 + exp(-alpha a)), a = mean X - K
+                                                         heston_dnnpde.py:551-556     */
+
+/* problem kinds */
+#define DBSDE_PROB_DIAG 0     /* mu = mu_a X, sigma = diag(sig_a X + sig_b)          */
+#define DBSDE_PROB_HESTON 1   /* k-asset Heston (heston_dnnpde.py:519-659), state
+                                 [S_1..S_k, v_1..v_k], one Brownian motion per asset */
 
 /*
  * Problem coefficients (one FBSNN subclass = one filled struct):
- *   mu(X)    = mu_a * X                                  (diagonal drift)
- *   sigma(X) = diag(sig_a * X + sig_b)                   (the reference's
+ *   kind DIAG:
+ *     mu(X)    = mu_a * X                                (diagonal drift)
+ *     sigma(X) = diag(sig_a * X + sig_b)                 (the reference's
  *                                                          dense diag_embed sigma)
+ *   kind HESTON (heston_dnnpde.py:587-605), per asset i, sv = sqrt(max(v_i, 1e-8)):
+ *     mu       = clamp([mu_a S_i, h_kappa (h_theta - v_i)], -100, 100)
+ *     Sigma_i  = clamp([[sv S_i, h_rho h_sigma sv], [h_rho sv S_i, h_sigma sv]], -100, 100)
+ *     driven by the asset's scalar dW_i (the reference's FBSNN dimension is 1;
+ *     its einsum broadcasts dW over both state components)
  *   phi      = phi_r * (Y - phi_c * X.Z) + phi_zz * |Z|^2
- *   g        = g_kind with strike
+ *   g        = g_kind over the first g_cols state columns (0 = all), strike,
+ *              g_alpha (DBSDE_G_SMOOTH_CALL); the terminal |Z - grad g|^2 term
+ *              runs over the same columns (heston_dnnpde.py:654: dU/dS only)
+ *   u_clamp  = 1: u = max(net(t, X), 0) (heston_dnnpde.py:568)
  *   q3       = 1: for D == 1 reproduce the reference's squeeze() broadcast in
  *              the Y-tilde term (1d_BSPDE_case.py:271-273)
  */
 typedef struct dbsde_problem {
+  int kind;
   float mu_a, sig_a, sig_b;
   float phi_r, phi_c, phi_zz;
   int g_kind;
   float strike;
   int q3;
+  int g_cols;
+  float g_alpha;
+  int u_clamp;
+  float h_kappa, h_theta, h_sigma, h_rho;
 } dbsde_problem;
 
 typedef struct dbsde_config {
@@ -98,15 +121,30 @@ long long dbsde_param_count(const dbsde_ctx* ctx);
  * Resnet(stable) input_layers[-1] is never used and stays grad=None) */
 int dbsde_param_used_mask(const dbsde_ctx* ctx, unsigned char* mask, long long n);
 
+/* Brownian dimension nb of a batch's W [M, N+1, nb]: D, or D/2 for Heston */
+int dbsde_brownian_dim(const dbsde_ctx* ctx);
+
+/*
+ * Cholesky factor of the increments' correlation matrix for the DEVICE mode
+ * (with_corr_high_dimension_pde.py:339-341: dW = L (sqrt(dt) z)).  L is a host
+ * [n, n] row-major lower-triangular fp32 matrix, n = dbsde_brownian_dim <= 128;
+ * the context keeps a device copy (staged in LDS by the path kernel).  L ==
+ * NULL clears it.  Parity-mode batches (W != NULL) already carry correlated W
+ * and ignore L.  DIAG problems only.
+ */
+int dbsde_set_corr(dbsde_ctx* ctx, const float* L, int n);
+
 /*
  * One minibatch (FBSNN.fetch_minibatch output, DeepBSDE.py:247-262).
- *   W != NULL : parity mode, t [M,N+1] and W [M,N+1,D] device fp32 exactly as
+ *   W != NULL : parity mode, t [M,N+1] and W [M,N+1,nb] device fp32 exactly as
  *               the reference builds them (cumsum in fp64, cast).
  *   W == NULL : device mode, Brownian increments sqrt(dt)*N(0,1) drawn by an
  *               in-kernel Philox4x32-10 keyed by (seed, offset, global path,
- *               step, dim); t == NULL means the uniform grid T*n/N.
+ *               step, Brownian coordinate), correlated by L when set;
+ *               t == NULL means the reference's grid fp32(cumsum_fp64(T/N)).
  *               A rank holding paths [path0, path0+M) of a larger batch draws
  *               exactly the increments a single device would draw for them.
+ *   Xi         : device [xi_rows, D] initial state (Heston: [S_1..S_k, v_1..v_k]).
  */
 typedef struct dbsde_batch {
   int M, N;
@@ -126,6 +164,16 @@ typedef struct dbsde_outputs {
 } dbsde_outputs;
 
 /*
+ * Device FBSNN.fetch_minibatch (DeepBSDE.py:247-262, with_corr...py:316-353)
+ * for a device-mode batch (batch->W must be NULL, batch->t NULL): writes t
+ * [M, N+1] and, with increments == 0, W [M, N+1, nb] = fp32(fp64 cumsum of dW)
+ * (the reference's layout), or with increments == 1 the raw dW
+ * [M, N, nb] the device-mode rollout consumes (correlated when
+ * dbsde_set_corr was called).
+ */
+int dbsde_brownian(dbsde_ctx* ctx, const dbsde_batch* batch, float* t, float* W, int increments);
+
+/*
  * FBSNN.loss_function + loss.backward (DeepBSDE.py:202-245, 279).
  * grad (device, flat, param_count) receives d loss / d params (overwritten,
  * 0 for unused parameters); grad == NULL runs the forward only (predict,
@@ -134,26 +182,70 @@ typedef struct dbsde_outputs {
 int dbsde_loss_grad(dbsde_ctx* ctx, const float* params, const dbsde_batch* batch,
                     float* grad, const dbsde_outputs* out);
 
-/* FBSNN.net_u (DeepBSDE.py:189-194): u [R] and Du [R,D] at R points. */
+/* FBSNN.net_u (DeepBSDE.py:189-194): u [R] and Du [R,D] at R points
+ * (Heston: the clamped u and its masked gradient, heston_dnnpde.py:560-579). */
 int dbsde_net_u(dbsde_ctx* ctx, const float* params, int R, const float* t,
                 const float* X, float* u, float* Du);
 
-/* optimizers (nd_BSPDE_case.py:331-350) */
+/* optimizers (nd_BSPDE_case.py:331-350), torch.optim single-tensor formula order */
 #define DBSDE_OPT_ADAM 0
 #define DBSDE_OPT_ADAMW 1
 #define DBSDE_OPT_SGD 2
+#define DBSDE_OPT_RMSPROP 3   /* state: v = square_avg                 */
+#define DBSDE_OPT_ADAGRAD 4   /* state: v = state_sum                  */
+#define DBSDE_OPT_ADAMAX 5    /* state: m = exp_avg, v = exp_inf       */
+#define DBSDE_OPT_ADADELTA 6  /* state: v = square_avg, m = acc_delta  */
+#define DBSDE_OPT_ASGD 7      /* state: m = ax (averaged parameters)   */
 
 typedef struct dbsde_optim {
   int kind;
   float lr, beta1, beta2, eps, weight_decay;
   float max_norm;    /* clip_grad_norm_(max_norm) before the step; <= 0: no clip */
   long long step;    /* 1-based step count of THIS update (bias correction) */
+  float alpha;       /* RMSprop smoothing constant (torch default 0.99) */
+  float rho;         /* Adadelta rho (0.9) */
+  float lr_decay;    /* Adagrad lr_decay (0) */
+  float lambd;       /* ASGD lambd (1e-4) */
+  float asgd_eta;    /* ASGD eta and mu of THIS step: torch keeps them as fp32 */
+  float asgd_mu;     /* state; the caller runs that recursion                   */
+  const float* loss; /* nullable device scalar: skip the update when it is not
+                        finite (heston_dnnpde.py:409-411 NaN skip)              */
 } dbsde_optim;
 
 /* clip_grad_norm_ + optimizer.step() (nd_BSPDE_case.py:383-384); m, v device
- * flat moments owned by the caller (zero-initialised for a fresh optimizer). */
+ * flat state owned by the caller (zero-initialised for a fresh optimizer). */
 int dbsde_optimizer_step(dbsde_ctx* ctx, float* params, float* grad, float* m, float* v,
                          const dbsde_optim* opt);
+
+/*
+ * Exact / comparator solutions on the device (the references' evaluators):
+ *   DBSDE_EXACT_BSB          u = exp((r + s^2)(T - t)) |x|^2    DeepBSDE.py:345-349
+ *                            (r, s = p[0], p[1])
+ *   DBSDE_EXACT_BS_CALL      Black-Scholes call price / delta of every coordinate
+ *                            (nd_BSPDE_case.py:587-618; r, sigma, K = p[0..2])
+ *   DBSDE_EXACT_BASKET_AVG   call on mean(x) with sigma / sqrt(D)
+ *                            (with_corr...py:663-700; r, sigma, K = p[0..2])
+ *   DBSDE_EXACT_BASKET_MEAN  mean over coordinates of the per-asset BS call
+ *                            (with_corr...py:621-660; r, sigma, K = p[0..2])
+ * t [R], x [R, D] device fp32; price and delta (nullable) [R * ncol],
+ * ncol = D for BS_CALL, 1 otherwise.  At t >= T the payoff and its 0 / 1/2 / 1
+ * delta are returned, as the references do.  Computed in fp64.
+ */
+#define DBSDE_EXACT_BSB 0
+#define DBSDE_EXACT_BS_CALL 1
+#define DBSDE_EXACT_BASKET_AVG 2
+#define DBSDE_EXACT_BASKET_MEAN 3
+int dbsde_exact(int kind, const float* t, const float* x, long long R, int D, float T, const double* params,
+                float* price, float* delta, void* hip_stream);
+
+/*
+ * HJB Monte-Carlo comparator (hjb_implement.py:1088-1095):
+ *   u(t, x) = -log( mean_k exp(-g(x + sqrt(2 |T - t|) z_k)) ),  g = log(1/2 + |y|^2/2)
+ * over mc Philox draws z_k keyed by (seed, point index); t [P], x [P, D],
+ * u [P] device.  Deterministic (fixed-order fp64 reduction).
+ */
+int dbsde_hjb_mc(const float* t, const float* x, int P, int D, float T, long long mc, unsigned long long seed,
+                 float* u, void* hip_stream);
 
 /* Per-kernel timing with HIP events on the context stream (bench/profiling). */
 int dbsde_profile_enable(dbsde_ctx* ctx, int enable);

@@ -22,7 +22,9 @@ What it restates (file:line into the reference snapshot):
   problems     DeepBSDE.py:326-341 (BSB), nd_BSPDE_case.py:503-539 (CallOption),
                1d_BSPDE_case.py:510-560 (1-D call), with_corr...:546-596
                (basket CallOption), with_corr...:599-616 (BSPDETestCase),
-               hjb_implement.py:590-604 (HJB)
+               hjb_implement.py:590-604 (HJB), heston_dnnpde.py:519-659 (Heston:
+               own net_u with the u clamp, own loss_function, k = 1 exactly as
+               the reference; k > 1 the per-asset generalisation)
   train step   nd_BSPDE_case.py:316-410 (N schedule, clip 1.0, Adam),
                DeepBSDE.py:265-295 (no schedule, no clip)
 """
@@ -405,6 +407,135 @@ def train(model, problem, Xi, M, N, D, T, n_iter, lr, clip=True, Mm=None,
     return losses, y0s
 
 
+# --------------------------------------------------------------------------
+# Heston (heston_dnnpde.py:519-659)
+# --------------------------------------------------------------------------
+
+
+def build_heston_model(mode, layers, activation, n_assets=1):
+    """heston_dnnpde.py:522-585: base FBSNN model on `layers` (input D+1,
+    default + xavier init), input-facing Linears replaced by (1 + 2k)-input
+    ones, then every parameter re-initialised (xavier gain 0.5 / zeros)."""
+    model = build_model(mode, layers, activation)
+    n_in = 1 + 2 * n_assets
+    if mode == "FC":
+        model[0] = nn.Linear(n_in, layers[1])
+    elif mode == "Naisnet":
+        model.layer1 = nn.Linear(n_in, layers[1])
+        model.layer2_input = nn.Linear(n_in, layers[2])
+        if len(layers) >= 5:
+            model.layer3_input = nn.Linear(n_in, layers[3])
+        if len(layers) == 6:
+            model.layer4_input = nn.Linear(n_in, layers[4])
+    else:
+        raise ValueError(mode)
+    for prm in model.parameters():
+        if len(prm.shape) > 1:
+            torch.nn.init.xavier_uniform_(prm, gain=0.5)
+        else:
+            torch.nn.init.zeros_(prm)
+    return model
+
+
+@dataclass
+class Heston:
+    k: int = 1
+    kappa: float = 2.0
+    theta: float = 0.2
+    sigma: float = 0.3
+    rho: float = 0.8
+    v0: float = 0.2
+    payoff: str = "discontinuous"
+    strike: float = 1.0
+
+    def g(self, S):
+        a = torch.mean(S, dim=1, keepdim=True) - self.strike if self.k > 1 else S - self.strike
+        if self.payoff == "discontinuous":
+            return torch.maximum(a, torch.tensor(0.0))
+        return a / (1 + torch.exp(-10.0 * a))
+
+
+def heston_net_u(model, t, X):
+    """heston_dnnpde.py:560-579: u = clamp(model(t, S, v), min 0), Du over (S, v)."""
+    u = model(torch.cat((t, X), 1))
+    u = torch.clamp(u, min=0.0)
+    du = torch.autograd.grad(outputs=u, inputs=X, grad_outputs=torch.ones_like(u), create_graph=True,
+                             retain_graph=True)[0]
+    return u, du
+
+
+def heston_loss_function(model, h, t, W, Xi, M):
+    """heston_dnnpde.py:611-659 per asset: X = [S_1..S_k, v_1..v_k], W [M, N+1, k].
+    For k = 1 every expression is the reference's, in its order."""
+    k = h.k
+    N = t.shape[1] - 1
+    t0, W0 = t[:, 0, :], W[:, 0, :]
+    Xi = Xi.reshape(-1, Xi.shape[-1])
+    S0 = Xi[:, :k].repeat(M, 1) if Xi.shape[0] == 1 else Xi[:, :k]
+    v0 = torch.full((M, k), h.v0)
+    X0 = torch.cat([S0, v0], dim=1)
+    Y0, Z0 = heston_net_u(model, t0, X0)
+    Xs, Ys, Zs = [X0], [Y0], [Z0]
+    loss = 0
+    for n in range(N):
+        t1, W1 = t[:, n + 1, :], W[:, n + 1, :]
+        dW = W1 - W0
+        S, v = X0[:, :k], X0[:, k:]
+        mu = torch.cat([0.05 * S, h.kappa * (h.theta - v)], dim=1).clamp(-100, 100)
+        sv = torch.sqrt(torch.clamp(v, min=1e-8))
+        sS, sV = sv * S, h.sigma * sv
+        d00, d11 = sS.clamp(-100, 100), sV.clamp(-100, 100)
+        d01, d10 = (h.rho * sV).clamp(-100, 100), (h.rho * sS).clamp(-100, 100)
+        X1 = X0 + mu * (t1 - t0) + torch.cat([(d00 + d01) * dW, (d10 + d11) * dW], dim=1)
+        a = d00 * dW + d01 * dW
+        b = d10 * dW + d11 * dW
+        Y1t = Y0 + 0.05 * Y0 * (t1 - t0) + torch.sum(Z0[:, :k] * a + Z0[:, k:] * b, dim=1, keepdim=True)
+        Y1, Z1 = heston_net_u(model, t1, X1)
+        loss = loss + torch.sum(torch.pow(Y1 - Y1t, 2))
+        t0, W0, X0, Y0, Z0 = t1, W1, X1, Y1, Z1
+        Xs.append(X0)
+        Ys.append(Y0)
+        Zs.append(Z0)
+    loss = loss + torch.sum(torch.pow(Y1 - h.g(X1[:, :k]), 2))
+    S1 = X1[:, :k]
+    g = h.g(S1)
+    dg = torch.autograd.grad(outputs=[g], inputs=[S1], grad_outputs=torch.ones_like(g), allow_unused=True,
+                             retain_graph=True, create_graph=True)[0]
+    loss = loss + torch.sum(torch.pow(Z1[:, :k] - dg, 2))
+    return loss, torch.stack(Xs, 1), torch.stack(Ys, 1), torch.stack(Zs, 1)
+
+
+def heston_loss_and_grads(model, h, t, W, Xi, M):
+    model.zero_grad(set_to_none=True)
+    xi = torch.as_tensor(Xi, dtype=torch.float32).clone().requires_grad_(True)   # the reference's Xi (:135)
+    loss, X, Y, Z = heston_loss_function(model, h, t, W, xi, M)
+    loss.backward()
+    g, mask = flat_grads(model)
+    return dict(loss=float(loss), X=X.detach().numpy(), Y=Y.detach().numpy(), Z=Z.detach().numpy(),
+                grad=g, used=mask)
+
+
+def heston_train(model, h, Xi, M, N, T, n_iter, lr, Mm=None, start_it=0):
+    """heston_dnnpde.py:345-450: N schedule, Adam, NaN skip, clip 1.0; the
+    minibatch has one Brownian column per asset (:309-343 with D = k)."""
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    losses = []
+    for it in range(start_it, start_it + n_iter):
+        if Mm is not None:
+            N = n_schedule(it, Mm, N)
+        opt.zero_grad()
+        t, W = fetch_minibatch(M, N, h.k, T)
+        xi = torch.as_tensor(Xi, dtype=torch.float32).clone().requires_grad_(True)
+        loss, X, Y, Z = heston_loss_function(model, h, t, W, xi, M)
+        if torch.isnan(loss):
+            continue
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+        opt.step()
+        losses.append(float(loss))
+    return losses
+
+
 def bsb_u_exact(t, X, T=1.0):
     """DeepBSDE.py:345-349 (the north-star known answer)."""
     r, smax = 0.05, 0.4
@@ -419,5 +550,7 @@ __all__ = [
     "SineAct", "ResnetRef", "NaisnetRef", "build_model", "flat_params", "set_flat_params",
     "flat_grads", "Problem", "make_problem", "fetch_minibatch", "net_u", "dg",
     "loss_function", "n_schedule", "loss_and_grads", "train", "bsb_u_exact", "param_count",
+    "build_heston_model", "Heston", "heston_net_u", "heston_loss_function", "heston_loss_and_grads",
+    "heston_train",
 ]
 

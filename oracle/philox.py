@@ -1,26 +1,30 @@
 """ORACLE -- test infrastructure only, never the product path.
 
-NumPy restatement of the device-mode Brownian increments and rollout of the
-HIP library (throughput mode, dbsde_batch.W == NULL; csrc/kernels.hpp
-philox_normal4, rollout_kernel, rollout_corr_kernel):
+NumPy restatement of the device-mode Brownian increments and path step of the
+HIP library (throughput mode, dbsde_batch.W == NULL; csrc/philox.hpp,
+csrc/paths.hpp rollout_kernel / rollout_corr_kernel / rollout_heston_kernel,
+dbsde_brownian):
 
   * Philox4x32-10 (Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as
     easy as 1, 2, 3", SC'11; the Random123 round constants), counter
-    (d, n/4, global path, offset), key (seed ^ offset_hi, seed_hi);
+    (d, n/4, global path, offset), key (seed ^ offset_hi, seed_hi), pinned by
+    the Random123 known-answer vectors (tests/test_oracle_philox.py);
   * Box-Muller on the two uniform pairs of one block: four N(0, 1) draws,
     the increments of steps n..n+3 of coordinate d;
   * dW = sqrt(dt) z, or the Cholesky-correlated dW = L (sqrt(dt) z) of
     with_corr_high_dimension_pde.py:334-341;
+  * the time grid of the reference's fetch_minibatch: t_n = fp32(fp64 cumsum
+    of T/N) (DeepBSDE.py:250-258);
   * the Euler-Maruyama rollout in the reference's operation order
-    (DeepBSDE.py:218-222 with sigma = diag(sig_a X + sig_b), mu = mu_a X), in
-    float32 like the kernel.
+    (DeepBSDE.py:218-222 with sigma = diag(sig_a X + sig_b), mu = mu_a X;
+    heston_dnnpde.py:629-642 for the k-asset Heston state), in float32 like
+    the kernel.
 
 The reference draws its increments from numpy's legacy normal stream
 (DeepBSDE.py:255); no device generator reproduces that stream, so the device
-mode is pinned here instead: the generator against the Random123 known-answer
-vectors (tests/test_oracle_philox.py), the device rollout against this
-restatement (tests/test_gpu_device_rng.py).  Also the HJB Monte-Carlo value
-(hjb_implement.py:1088-1095) on the same draws as the device comparator.
+mode is pinned here instead (tests/test_gpu_device_rng.py).  Also the HJB
+Monte-Carlo value (hjb_implement.py:1088-1095) on the same draws as the
+device comparator (csrc/evals.hip hjb_mc_kernel).
 """
 from __future__ import annotations
 
@@ -29,7 +33,7 @@ import numpy as np
 _M0, _M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
 _W0, _W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
 _LO = np.uint64(0xFFFFFFFF)
-HJB_TAG = 0x484A42          # kernels.hpp hjb_mc_kernel counter word
+HJB_TAG = 0x484A42          # csrc/evals.hip hjb_mc_kernel counter word
 
 
 def philox4x32_10(ctr, key):
@@ -77,23 +81,64 @@ def increments(seed, offset, path0, M, N, D, T, L=None):
     return dw
 
 
+def time_grid(N, T):
+    """t_n = fp32(fp64 cumsum of T/N), the reference's fetch_minibatch grid."""
+    return np.concatenate([[0.0], np.cumsum(np.full(N, T / N))]).astype(np.float32)
+
+
+def brownian_W(dw):
+    """W [M, N+1, nb] = fp32(fp64 cumsum of dW) with W_0 = 0 (dbsde_brownian)."""
+    M, N, nb = dw.shape
+    W = np.zeros((M, N + 1, nb))
+    W[:, 1:] = np.cumsum(dw.astype(np.float64), axis=1)
+    return W.astype(np.float32)
+
+
 def rollout(Xi, dw, T, mu_a=0.0, sig_a=0.0, sig_b=0.0):
-    """X [M, N+1, D] float32: x1 = (x + (mu_a x) dt) + (sig_a x + sig_b) dw,
-    uniform grid t_n = float(T n / N) (the kernel's t == NULL grid)."""
+    """X [M, N+1, D] float32: x1 = (x + (mu_a x) dt) + (sig_a x + sig_b) dw on the
+    reference grid."""
     M, N, D = dw.shape
     f32 = np.float32
     x = np.broadcast_to(np.asarray(Xi, f32).reshape(-1, D), (M, D)).astype(f32)
     X = np.empty((M, N + 1, D), f32)
-    t0 = f32(0.0)
+    tg = time_grid(N, T)
     for n in range(N):
         X[:, n] = x
-        t1 = f32(float(f32(T)) * (n + 1) / N)
-        dt = f32(t1 - t0)
+        dt = f32(tg[n + 1] - tg[n])
         s = (f32(sig_a) * x + f32(sig_b)) * dw[:, n]
         x = (x + (f32(mu_a) * x) * dt) + s
-        t0 = t1
     X[:, N] = x
     return X
+
+
+def heston_rollout(Xi, dw, T, mu_a=0.05, kappa=2.0, theta=0.2, sigma=0.3, rho=0.8):
+    """k-asset Heston state [S_1..S_k, v_1..v_k] (heston_dnnpde.py:587-605,
+    629-642): mu and the diffusion blocks clamped to [-100, 100], one dW per
+    asset; the X update uses (Sig_i0 + Sig_i1) dW (torch.einsum sums the
+    broadcast dimension first).  Returns X [M, N+1, 2k] and the Y-tilde vector
+    sdw [M, N, 2k] = (Sig_i0 dW + Sig_i1 dW)."""
+    M, N, k = dw.shape
+    f32 = np.float32
+    x = np.broadcast_to(np.asarray(Xi, f32).reshape(-1, 2 * k), (M, 2 * k)).astype(f32)
+    S, v = x[:, :k].copy(), x[:, k:].copy()
+    X = np.empty((M, N + 1, 2 * k), f32)
+    sdw = np.empty((M, N, 2 * k), f32)
+    tg = time_grid(N, T)
+    c = lambda a: np.clip(a, f32(-100), f32(100))
+    for n in range(N):
+        X[:, n, :k], X[:, n, k:] = S, v
+        dt = f32(tg[n + 1] - tg[n])
+        muS, muV = c(f32(mu_a) * S), c(f32(kappa) * (f32(theta) - v))
+        sv = np.sqrt(np.maximum(v, f32(1e-8)))
+        sS, sV = sv * S, f32(sigma) * sv
+        d00, d11, d01, d10 = c(sS), c(sV), c(f32(rho) * sV), c(f32(rho) * sS)
+        w = dw[:, n]
+        sdw[:, n, :k] = d00 * w + d01 * w
+        sdw[:, n, k:] = d10 * w + d11 * w
+        S = (S + muS * dt) + (d00 + d01) * w
+        v = (v + muV * dt) + (d10 + d11) * w
+    X[:, N, :k], X[:, N, k:] = S, v
+    return X, sdw
 
 
 def hjb_value(t, X, T, mc, seed):
@@ -113,4 +158,5 @@ def hjb_value(t, X, T, mc, seed):
     return out[:, None]
 
 
-__all__ = ["philox4x32_10", "normal4", "increments", "rollout", "hjb_value", "HJB_TAG"]
+__all__ = ["philox4x32_10", "normal4", "increments", "time_grid", "brownian_W", "rollout", "heston_rollout",
+           "hjb_value", "HJB_TAG"]

@@ -15,7 +15,8 @@ implement -- derived by hand from the reference graph:
   * d/dtheta [ubar*u + zbar.grad_x u] = reverse mode over (primal forward +
     forward tangent along zbar) -- SURVEY 3.3.
 
-Checked against fbsnn_ref (autograd double backward) in tests/test_timeparallel.py.
+Checked against the reference's golden vectors in tests/test_oracle_golden.py
+(and thereby against fbsnn_ref's autograd double backward).
 
 Unified network ("blocks"): every supported mode is
     h_1 = act(x W_in^T + b_in)
@@ -162,6 +163,9 @@ PROBLEMS = {
 }
 
 
+HESTON_DEFAULTS = dict(kappa=2.0, theta=0.2, sigma=0.3, rho=0.8, v0=0.2, payoff="discontinuous")
+
+
 def g_and_grad(kind, X, strike):
     if kind == "sumsq":
         return np.sum(X * X, 1), 2.0 * X
@@ -174,7 +178,33 @@ def g_and_grad(kind, X, strike):
     if kind == "log":
         q = 0.5 + 0.5 * np.sum(X * X, 1)
         return np.log(q), X / q[:, None]
+    if kind == "smooth_call":       # heston_dnnpde.py:551-556: a / (1 + e^{-10 a}), a = mean X - K
+        a = np.mean(X, 1) - strike
+        e = np.exp(-10.0 * a)
+        d = (1.0 / (1.0 + e) + a * 10.0 * e / (1.0 + e) ** 2) / X.shape[1]
+        return a / (1.0 + e), np.repeat(d[:, None], X.shape[1], 1)
     raise ValueError(kind)
+
+
+def heston_rollout(t, W, Xi, kappa, theta, sigma, rho, **_):
+    """heston_dnnpde.py:629-642 (fp64): state [S_1..S_k, v_1..v_k], W [M, N+1, k];
+    sdw is the vector the Y-tilde term contracts with Z."""
+    M, N1, k = W.shape
+    X = np.zeros((M, N1, 2 * k))
+    X[:, 0] = Xi if Xi.shape[0] == M else np.repeat(Xi.reshape(1, 2 * k), M, 0)
+    sdw = np.zeros((M, N1 - 1, 2 * k))
+    c = lambda a: np.clip(a, -100.0, 100.0)
+    for n in range(N1 - 1):
+        S, v = X[:, n, :k], X[:, n, k:]
+        dt = (t[:, n + 1] - t[:, n])[:, None]
+        w = W[:, n + 1] - W[:, n]
+        sv = np.sqrt(np.maximum(v, 1e-8))
+        d00, d11, d01, d10 = c(sv * S), c(sigma * sv), c(rho * sigma * sv), c(rho * sv * S)
+        sdw[:, n, :k] = (d00 + d01) * w
+        sdw[:, n, k:] = (d10 + d11) * w
+        X[:, n + 1, :k] = S + c(0.05 * S) * dt + sdw[:, n, :k]
+        X[:, n + 1, k:] = v + c(kappa * (theta - v)) * dt + sdw[:, n, k:]
+    return X, sdw
 
 
 def rollout(problem, t, W, Xi):
@@ -198,22 +228,35 @@ def rollout(problem, t, W, Xi):
 # --------------------------------------------------------------------------
 
 
-def loss_grad(flat, mode, layers, activation, problem, t, W, Xi, strike=None, q3=True):
+def loss_grad(flat, mode, layers, activation, problem, t, W, Xi, strike=None, q3=True, heston=None):
     """Returns dict(loss, X, Y, Z, grad) with grad in state_dict order (unused
-    Q6 parameters get 0)."""
+    Q6 parameters get 0).  problem == "heston": the k-asset Heston problem
+    (heston_dnnpde.py:519-659) with parameters `heston` (HESTON_DEFAULTS), Xi
+    the full initial state [S, v], W [M, N+1, k]."""
     P = unpack(flat, mode, layers)
     nm = _names(mode, layers)
     sig, d1, d2 = act_fns(activation)
-    mu_a, sig_a, sig_b, phi_r, phi_c, phi_zz, gk = PROBLEMS[problem]
     D = layers[0] - 1
-    if strike is None:
-        strike = {"call": 1.0 * D, "call1d": 1.0 * D, "basket": 1.0}.get(problem, 0.0)
     t = np.asarray(t)
     if t.ndim == 3:
         t = t[:, :, 0]
     M, N1, _ = W.shape
     N = N1 - 1
-    X, sdw = rollout(problem, t[:, :, None], W, Xi)
+    clamp = problem == "heston"
+    if clamp:
+        hp = dict(HESTON_DEFAULTS, **(heston or {}))
+        mu_a, sig_a, sig_b, phi_r, phi_c, phi_zz = 0.05, 0.0, 0.0, 0.05, 0.0, 0.0
+        gk = "call_mean" if hp["payoff"] == "discontinuous" else "smooth_call"
+        G = D // 2
+        strike = 1.0 if strike is None else strike
+        X, sdw = heston_rollout(t, W, Xi, **hp)
+        q3 = False
+    else:
+        mu_a, sig_a, sig_b, phi_r, phi_c, phi_zz, gk = PROBLEMS[problem]
+        G = D
+        if strike is None:
+            strike = {"call": 1.0 * D, "call1d": 1.0 * D, "basket": 1.0}.get(problem, 0.0)
+        X, sdw = rollout(problem, t[:, :, None], W, Xi)
     R = M * N1
     x = np.concatenate([t.reshape(R, 1), X.reshape(R, D)], 1)          # [R, D+1]
 
@@ -245,6 +288,10 @@ def loss_grad(flat, mode, layers, activation, problem, t, W, Xi, strike=None, q3
         a.append(ak)
         h.append(sig(ak) + rho * h[k + 1])     # h[k+2] = h_{k+2}
     u = h[K + 1] @ wout + bout
+    umask = np.ones_like(u)
+    if clamp:                                   # heston_dnnpde.py:568, clamp passes the gradient at 0
+        umask = (u >= 0).astype(u.dtype)
+        u = u * umask
 
     # ---- input gradient (delta[k] pairs with a[k])
     g = [None] * (K + 2)
@@ -258,7 +305,7 @@ def loss_grad(flat, mode, layers, activation, problem, t, W, Xi, strike=None, q3
     for k in range(1, K + 1):
         if Vs[k - 1] is not None:
             zfull = zfull + delta[k] @ Vs[k - 1]
-    Z = zfull[:, 1:]
+    Z = zfull[:, 1:] * umask[:, None]
 
     # ---- residuals and cotangents
     Y = u.reshape(M, N1)
@@ -273,9 +320,9 @@ def loss_grad(flat, mode, layers, activation, problem, t, W, Xi, strike=None, q3
     phi = phi_r * (Y[:, :-1] - phi_c * s_xz) + phi_zz * s_zz
     ytil = Y[:, :-1] + phi * dt + s_zs
     r = Y[:, 1:] - ytil                                             # [M, N]
-    gT, dgT = g_and_grad(gk, X[:, -1], strike)
+    gT, dgT = g_and_grad(gk, X[:, -1, :G], strike)
     rT = Y[:, -1] - gT
-    zT = Zr[:, -1] - dgT
+    zT = Zr[:, -1, :G] - dgT
     loss = np.sum(r * r) + np.sum(rT * rT) + np.sum(zT * zT)
 
     ubar = np.zeros((M, N1))
@@ -289,8 +336,9 @@ def loss_grad(flat, mode, layers, activation, problem, t, W, Xi, strike=None, q3
     else:
         dsz = sdw
     zb[:, :-1] = -2 * r[:, :, None] * (dphidz * dt[:, :, None] + dsz)
-    zb[:, -1] = 2 * zT
-    ub = ubar.reshape(R)
+    zb[:, -1, :G] = 2 * zT
+    ub = ubar.reshape(R) * umask
+    zb = zb * umask.reshape(M, N1, 1)
     zbar = np.concatenate([np.zeros((R, 1)), zb.reshape(R, D)], 1)   # t-component 0
 
     # ---- forward tangent along zbar
@@ -329,5 +377,5 @@ def loss_grad(flat, mode, layers, activation, problem, t, W, Xi, strike=None, q3
     return dict(loss=loss, X=X, Y=Y[:, :, None], Z=Zr, grad=flatg, ubar=ub, zbar=zbar, r=r)
 
 
-__all__ = ["param_layout", "unpack", "act_fns", "project", "project_vjp", "PROBLEMS",
-           "g_and_grad", "rollout", "loss_grad"]
+__all__ = ["param_layout", "unpack", "act_fns", "project", "project_vjp", "PROBLEMS", "HESTON_DEFAULTS",
+           "g_and_grad", "rollout", "heston_rollout", "loss_grad"]

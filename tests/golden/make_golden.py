@@ -48,6 +48,7 @@ def _setup():
         corr=_load("with_corr_high_dimension_pde.py", "ref_corr"),
         hjb=_load("hjb_implement.py", "ref_hjb"),
         oned=_load("1d_BSPDE_case.py", "ref_1d"),
+        heston=_load("heston_dnnpde.py", "ref_heston"),
     )
     import torch
     torch.autograd.set_detect_anomaly(False)   # DeepBSDE.py:11 turns it on (Q8); speed only
@@ -157,6 +158,125 @@ def small_cases(mods):
         print(f"{name:42s} loss={res['loss']:.6e}")
 
 
+def _save_case(name, prob, mode, act, layers, Xi, M, N, seed, params, res, **extra):
+    np.savez_compressed(os.path.join(OUT, f"g1_{name}.npz"), name=name, problem=prob, mode=mode, activation=act,
+                        layers=np.array(layers), Xi=np.asarray(Xi, np.float32), M=M, N=N, T=1.0, seed=seed,
+                        params=params, **res, **extra)
+    print(f"{name:42s} loss={res['loss']:.6e}", flush=True)
+
+
+def wide_cases(mods):
+    """Round 2: the north-star width (fused T=7 kernels) for ReLU / Tanh, the
+    Q4 not-taken branch, config 3 (basket D=100 + Cholesky L, Naisnet-ReLU) and
+    config 4 (HJB FC-Sine [101,256x4,1], N=20) at small M."""
+    import torch
+    D = 100
+    L110 = [D + 1] + 4 * [110] + [1]
+    xi_bsb = np.array([1.0, 0.5] * (D // 2))[None, :]
+    specs = [
+        ("w110_deep_bsb_NAIS-Net_ReLU", "deep", "BlackScholesBarenblatt", "bsb", "NAIS-Net", "ReLU", L110, xi_bsb,
+         16, 5, {}),
+        ("w110_nd_call_Naisnet_Tanh", "nd", "CallOption", "call", "Naisnet", "Tanh", L110, np.ones((1, D)), 16, 5,
+         {"Mm": 5.0}),
+        ("w110_corr_basket_Naisnet_ReLU", "corr", "CallOption", "basket", "Naisnet", "ReLU", L110, np.ones((1, D)),
+         16, 5, {"Mm": 5.0, "correlation_type": "random_correlation"}),
+        ("w256_hjb_FC_Sine_N20", "hjb", "HamiltonJacobiBellman", "hjb", "FC", "Sine", [D + 1] + 4 * [256] + [1],
+         np.zeros((1, D)), 16, 20, {}),
+        ("q4off_deep_bsb_NAIS-Net_Sine", "deep", "BlackScholesBarenblatt", "bsb", "NAIS-Net", "Sine",
+         [5, 16, 16, 16, 16, 1], np.array([1.0, 0.5] * 2)[None, :], 8, 5, {"scale_hidden": 0.05}),
+        ("q4off_nd_call_Naisnet_Tanh", "nd", "CallOption", "call", "Naisnet", "Tanh", [5, 16, 16, 16, 1],
+         np.ones((1, 4)), 8, 5, {"Mm": 5.0, "scale_hidden": 0.05}),
+    ]
+    for k, (name, modkey, cls, prob, mode, act, layers, Xi, M, N, kw) in enumerate(specs):
+        seed = 300 + k
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        C = getattr(mods[modkey], cls)
+        Dd = layers[0] - 1
+        with contextlib.redirect_stdout(io.StringIO()):
+            if modkey in ("deep", "hjb"):
+                obj = C(Xi, 1.0, M, N, Dd, layers, mode, act)
+            elif modkey == "corr":
+                obj = C(Xi, 1.0, M, N, Dd, kw["Mm"], layers, mode, act, kw.get("correlation_type", "no_correlation"))
+            else:
+                obj = C(Xi, 1.0, M, N, Dd, kw["Mm"], layers, mode, act)
+        extra = {}
+        if "scale_hidden" in kw:        # drive |W^T W|_F below 0.98: the Q4 branch is not taken
+            with torch.no_grad():
+                norms = []
+                for name_, prm in obj.model.named_parameters():
+                    hidden = name_.startswith("hidden_layers.") or (name_.startswith("layer") and "_input" not in name_
+                                                                    and name_.split(".")[0] not in ("layer1",)
+                                                                    and name_.split(".")[0] != f"layer{len(layers) - 1}")
+                    if hidden and name_.endswith("weight"):
+                        prm.mul_(kw["scale_hidden"])
+                        norms.append(float(torch.norm(prm.t() @ prm)))
+            assert norms and max(norms) < 0.98, norms
+            extra["rtr_norms"] = np.array(norms)
+        params = _flat(obj.model.state_dict())
+        res = _run_case(obj, M, N, Dd)
+        if modkey in ("corr", "hjb"):
+            extra["corr"] = np.asarray(obj.correlation_matrix, np.float64)
+        _save_case(name, prob, mode, act, layers, Xi, M, N, seed, params, res, **extra)
+
+
+def _heston_run(obj, M, N):
+    """Reference Heston minibatch + loss + backward; Z = (dU/dS, dU/dv) from its net_u."""
+    import torch
+    with contextlib.redirect_stdout(io.StringIO()):
+        t, W = obj.fetch_minibatch()
+        obj.model.zero_grad(set_to_none=True)
+        loss, X, Y, _ = obj.loss_function(t, W, obj.Xi)
+        loss.backward()
+        g, used = _grads(obj.model)
+        Zs = []
+        for n in range(N + 1):
+            Xn = X[:, n, :].detach().clone().requires_grad_(True)
+            _, zs, zv = obj.net_u(t[:, n, :], Xn)
+            Zs.append(torch.cat([zs, zv], 1).detach())
+    return dict(t=t.numpy(), W=W.numpy(), loss=np.float64(loss.item()), X=X.detach().numpy(),
+                Y=Y.detach().numpy(), grad=g, used=used, Z=torch.stack(Zs, 1).numpy())
+
+
+def heston_cases(mods):
+    """Config 5 at the reference's only scope, one asset (heston_dnnpde.py:519-659):
+    loss/grad fixtures for both payoffs and both modes, and a 10-iteration train()."""
+    import torch
+    H = mods["heston"].HestonFBSNN
+    layers = [2, 16, 16, 16, 16, 1]
+    hp = dict(kappa=2.0, theta=0.2, sigma=0.3, rho=0.8, v0=0.2)
+    specs = [("heston_Naisnet_Sine", "Naisnet", "Sine", "discontinuous", 8, 5),
+             ("heston_Naisnet_Tanh_continuous", "Naisnet", "Tanh", "continuous", 8, 5),
+             ("heston_FC_Sine", "FC", "Sine", "discontinuous", 6, 4)]
+    for k, (name, mode, act, payoff, M, N) in enumerate(specs):
+        seed = 400 + k
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        Xi = np.array([[1.0]])
+        with contextlib.redirect_stdout(io.StringIO()):
+            obj = H(Xi, 1.0, M, N, 1, 5.0, layers, mode, act, payoff_type=payoff, **hp)
+        params = _flat(obj.model.state_dict())
+        res = _heston_run(obj, M, N)
+        _save_case(name, "heston", mode, act, [3] + layers[1:], Xi, M, N, seed, params, res,
+                   Xi_full=np.array([[1.0, hp["v0"]]], np.float32), payoff=payoff, **hp)
+    # train(): N schedule (Mm = 5 -> N = 5), clip 1.0, Adam, NaN skip
+    torch.manual_seed(450)
+    np.random.seed(450)
+    with contextlib.redirect_stdout(io.StringIO()):
+        obj = H(np.array([[1.0]]), 1.0, 8, 5, 1, 5.0, layers, "Naisnet", "Sine", **hp)
+    p0 = _flat(obj.model.state_dict())
+    np.random.seed(451)
+    with contextlib.redirect_stdout(io.StringIO()):
+        graph = obj.train(10, 1e-3)
+    p1 = _flat(obj.model.state_dict())
+    np.savez_compressed(os.path.join(OUT, "g1_train_heston_Naisnet_Sine.npz"), name="train_heston_Naisnet_Sine",
+                        problem="heston", mode="Naisnet", activation="Sine", layers=np.array([3] + layers[1:]),
+                        Xi=np.array([[1.0]], np.float32), Xi_full=np.array([[1.0, hp["v0"]]], np.float32), M=8,
+                        N=5, T=1.0, Mm=5.0, iters=10, lr=1e-3, batch_seed=451, clip=True, params0=p0, params1=p1,
+                        graph=np.asarray(graph), payoff="discontinuous", **hp)
+    print(f"{'train_heston_Naisnet_Sine':42s} |dp|={np.abs(p1 - p0).max():.3e}", flush=True)
+
+
 def train_cases(mods):
     """Reference train() trajectories: DeepBSDE (no clip) and nd (clip 1.0, Mm)."""
     import torch
@@ -254,8 +374,14 @@ if __name__ == "__main__":
     if "--trajectory-only" in sys.argv:
         north_star_trajectory(m)
         sys.exit(0)
+    if "--round2-only" in sys.argv:
+        wide_cases(m)
+        heston_cases(m)
+        sys.exit(0)
     small_cases(m)
     train_cases(m)
+    wide_cases(m)
+    heston_cases(m)
     if "--skip-north-star" not in sys.argv:
         north_star(m)
         north_star_trajectory(m)

@@ -43,7 +43,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 def test_abi_version_and_config_validation(lib):
     pkg = load_pkg()
-    assert lib.dbsde_abi_version() == 1
+    assert lib.dbsde_abi_version() == pkg._lib.ABI_VERSION == 2
     cfg = pkg._lib.Config()
     cfg.mode, cfg.activation, cfg.n_layers = 1, 0, 2          # too few layers -> EINVAL before any HIP call
     ctx = ctypes.c_void_p()
@@ -74,6 +74,8 @@ int main(void) {
   F(dbsde_config, problem) F(dbsde_config, T) F(dbsde_config, device)
   F(dbsde_batch, seed) F(dbsde_batch, path0) F(dbsde_batch, Xi) F(dbsde_batch, xi_rows)
   F(dbsde_optim, max_norm) F(dbsde_optim, step) F(dbsde_problem, q3)
+  F(dbsde_problem, kind) F(dbsde_problem, g_cols) F(dbsde_problem, u_clamp) F(dbsde_problem, h_rho)
+  F(dbsde_optim, alpha) F(dbsde_optim, asgd_mu) F(dbsde_optim, loss)
   return 0;
 }
 '''
@@ -96,6 +98,35 @@ def test_struct_layouts_match_ctypes(tmp_path):
             "dbsde_config.device": L.Config.device, "dbsde_batch.seed": L.Batch.seed,
             "dbsde_batch.path0": L.Batch.path0, "dbsde_batch.Xi": L.Batch.Xi,
             "dbsde_batch.xi_rows": L.Batch.xi_rows, "dbsde_optim.max_norm": L.Optim.max_norm,
-            "dbsde_optim.step": L.Optim.step, "dbsde_problem.q3": L.Problem.q3}
+            "dbsde_optim.step": L.Optim.step, "dbsde_problem.q3": L.Problem.q3,
+            "dbsde_problem.kind": L.Problem.kind, "dbsde_problem.g_cols": L.Problem.g_cols,
+            "dbsde_problem.u_clamp": L.Problem.u_clamp, "dbsde_problem.h_rho": L.Problem.h_rho,
+            "dbsde_optim.alpha": L.Optim.alpha, "dbsde_optim.asgd_mu": L.Optim.asgd_mu,
+            "dbsde_optim.loss": L.Optim.loss}
     for k, field in offs.items():
         assert int(got[k]) == field.offset, k
+
+
+def test_evaluator_entry_points_validate_before_any_hip_call(lib):
+    """dbsde_exact / dbsde_hjb_mc reject bad arguments with EINVAL (no GPU here)."""
+    pkg = load_pkg()
+    assert lib.dbsde_exact(9, None, None, 1, 1, 1.0, None, None, None, None) == pkg._lib.DBSDE_EINVAL
+    assert lib.dbsde_hjb_mc(None, None, 1, 1, 1.0, 10, 0, None, None) == pkg._lib.DBSDE_EINVAL
+    assert lib.dbsde_brownian_dim(None) == -1
+
+
+def test_problem_kind_validation(lib):
+    """Unknown problem kinds / terminal conditions and an odd Heston state are EINVAL."""
+    pkg = load_pkg()
+    cfg = pkg._lib.Config()
+    for k, v in enumerate([6, 16, 16, 16, 16, 1]):
+        cfg.layers[k] = v
+    cfg.mode, cfg.activation, cfg.n_layers = 3, 0, 6
+    ctx = ctypes.c_void_p()
+    cfg.problem.kind = 7
+    assert lib.dbsde_create(ctypes.byref(cfg), ctypes.byref(ctx)) == pkg._lib.DBSDE_EINVAL
+    cfg.problem.kind, cfg.problem.g_kind = 0, 9
+    assert lib.dbsde_create(ctypes.byref(cfg), ctypes.byref(ctx)) == pkg._lib.DBSDE_EINVAL
+    cfg.problem.kind, cfg.problem.g_kind = 1, 2                 # Heston with an odd state dimension (5)
+    assert lib.dbsde_create(ctypes.byref(cfg), ctypes.byref(ctx)) == pkg._lib.DBSDE_EINVAL
+    assert b"even" in lib.dbsde_last_error(None)

@@ -1,7 +1,11 @@
-"""Two ranks (gloo, both on cuda:0) running the native throughput step
-(device Philox increments keyed by the GLOBAL path index, [grad|loss]
-all-reduce, replicated Adam) must reproduce the single-process step over the
-same global batch.  Needs a GPU; RCCL itself is exercised by the bench at N>1."""
+"""Two ranks (gloo, both on cuda:0) running the native step must reproduce the
+single-process step over the same global batch:
+  * throughput mode: device Philox increments keyed by the GLOBAL path index,
+    [grad|loss] all-reduce, replicated Adam (what bench.py times);
+  * parity mode: the reference's train() loop, every rank drawing the global
+    numpy batch and uploading only its slice of paths.
+Needs a GPU.  RCCL (the "nccl" backend) needs one device per rank and is
+exercised by the driver's multi-GPU bench; a one-GPU box can only run gloo."""
 import os
 import socket
 
@@ -36,31 +40,53 @@ def _steps(m, k=3):
     return m.params.cpu().numpy(), losses
 
 
-def _worker(rank, world, port, q):
+def _train(m, k=3):
+    np.random.seed(5)
+    m.train(k, 1e-3)
+    torch.cuda.synchronize()
+    return m.params.cpu().numpy(), list(m.training_loss)
+
+
+def _worker(rank, world, port, q, what):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank,) + _steps(_model(world, rank)))
+        m = _model(world, rank)
+        q.put((rank,) + (_steps(m) if what == "steps" else _train(m)))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_ranks_match_one_process():
+def _two_ranks(what):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, what)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+def test_two_ranks_train_parity_mode_matches_one_process():
+    res = _two_ranks("train")
+    p1, l1 = _train(_model(1, 0))
+    (_, pa, la), (_, pb, lb) = res
+    np.testing.assert_array_equal(pa, pb)
+    np.testing.assert_allclose(la, l1, rtol=1e-5)
+    np.testing.assert_allclose(pa, p1, rtol=0, atol=2e-6)
+
+
+def test_two_ranks_match_one_process():
+    res = _two_ranks("steps")
     p1, l1 = _steps(_model(1, 0))
     (_, pa, la), (_, pb, lb) = res
     np.testing.assert_array_equal(pa, pb)                       # replicas identical

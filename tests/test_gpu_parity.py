@@ -29,8 +29,13 @@ def _load(p):
     return {k: z[k] for k in z.files}
 
 
-def spec_for(pkg, problem, D):
+def spec_for(pkg, problem, D, g=None):
     S = pkg.ProblemSpec
+    if problem == "heston":
+        smooth = str(g["payoff"]) == "continuous"
+        return S(kind="heston", mu_a=0.05, phi_r=0.05, g="smooth_call" if smooth else "call_mean", strike=1.0,
+                 g_alpha=10.0, g_cols=D // 2, u_clamp=True, q3=False, kappa=float(g["kappa"]),
+                 theta=float(g["theta"]), sigma=float(g["sigma"]), rho=float(g["rho"]))
     return {
         "bsb": S(sig_a=0.4, phi_r=0.05, phi_c=1.0, g="sumsq"),
         "bspde_test": S(mu_a=0.05, sig_a=0.2, phi_r=0.05, phi_c=1.0, g="sumsq"),
@@ -52,19 +57,17 @@ def dev():
     return torch.device("cuda:0")
 
 
-def make_solver(pkg, dev, g, fused=True, tnw=True, phase=None):
+def make_solver(pkg, dev, g, fused=True, tnw=True):
     """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at
     create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0)."""
     layers = [int(v) for v in g["layers"]]
     D = layers[0] - 1
     env = {"DBSDE_FUSED": "1" if fused else "0", "DBSDE_TNW": "1" if tnw else "0"}
-    if phase is not None:
-        env["DBSDE_PHASE"] = str(phase)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
-        return pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]), spec_for(pkg, str(g["problem"]), D),
-                                float(g["T"]), dev)
+        return pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]),
+                                spec_for(pkg, str(g["problem"]), D, g), float(g["T"]), dev)
     finally:
         for k, v in old.items():
             if v is None:
@@ -81,7 +84,8 @@ def native_case(pkg, dev, g, want_grad=True, fused=True):
     out = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (N + 1) * D, device=dev),
                Y=torch.empty(M * (N + 1), device=dev), Z=torch.empty(M * (N + 1) * D, device=dev))
     grad = torch.empty_like(params) if want_grad else None
-    s.loss_grad(params, M, N, torch.from_numpy(g["Xi"]).to(dev).contiguous(),
+    xi = g["Xi_full"] if "Xi_full" in g else g["Xi"]
+    s.loss_grad(params, M, N, torch.from_numpy(xi).to(dev).contiguous(),
                 t=torch.from_numpy(g["t"]).to(dev).reshape(M, N + 1).contiguous(),
                 W=torch.from_numpy(g["W"]).to(dev).contiguous(), grad=grad, **out)
     torch.cuda.synchronize()
@@ -136,6 +140,26 @@ def test_train_deepbsde_surface_matches_reference(pkg, dev):
     np.random.seed(int(g["batch_seed"]))
     graph = m.train(int(g["iters"]), float(g["lr"]))
     assert graph.shape[0] == 2
+    np.testing.assert_allclose(m.params.cpu().numpy(), g["params1"], rtol=0, atol=5e-5)
+
+
+def test_q4_not_taken_fixtures_exist():
+    """DESIGN Q4: both projection branches are exercised (taken by every Xavier
+    init, not taken by the rescaled fixtures in this list)."""
+    z = [p for p in G1 if "q4off" in p]
+    assert len(z) >= 2 and all(np.load(p)["rtr_norms"].max() < 0.98 for p in z)
+
+
+def test_train_heston_surface_matches_reference(pkg, dev):
+    """HestonFBSNN.train (heston_dnnpde.py:345-450: Mm schedule, clip 1.0, Adam,
+    NaN skip) for 10 iterations from the reference's params and numpy stream."""
+    g = _load(os.path.join(GOLDEN, "g1_train_heston_Naisnet_Sine.npz"))
+    m = pkg.HestonFBSNN(g["Xi"], float(g["T"]), int(g["M"]), int(g["N"]), 1, float(g["Mm"]),
+                        [2] + [int(v) for v in g["layers"]][1:], str(g["mode"]), str(g["activation"]), device=dev)
+    m.params.copy_(torch.from_numpy(g["params0"]).to(dev))
+    np.random.seed(int(g["batch_seed"]))
+    graph = m.train(int(g["iters"]), float(g["lr"]))
+    assert graph.shape[1] == 3          # [iteration, training_loss, Y0] (heston_dnnpde.py:448)
     np.testing.assert_allclose(m.params.cpu().numpy(), g["params1"], rtol=0, atol=5e-5)
 
 
@@ -217,7 +241,7 @@ def test_net_u_matches_fixture_Y(pkg, dev):
     g = _load(G1[0])
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
-    s = pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]), spec_for(pkg, str(g["problem"]), D),
+    s = pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]), spec_for(pkg, str(g["problem"]), D, g),
                          float(g["T"]), dev)
     params = torch.from_numpy(g["params"]).to(dev)
     R = M * (N + 1)
@@ -231,8 +255,7 @@ def test_net_u_matches_fixture_Y(pkg, dev):
     np.testing.assert_allclose(du.cpu().numpy(), g["Z"].reshape(R, D), rtol=0, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False), dict(phase=2)],
-                         ids=["chain", "splitk_weight_grad", "phase2_8wave"])
+@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False)], ids=["chain", "splitk_weight_grad"])
 def test_kernel_paths_agree_at_north_star(pkg, dev, variant):
     """The default kernels (fused phases + wave-owned weight-gradient tiles)
     against the per-layer chain path and against the split-K weight-gradient

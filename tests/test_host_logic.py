@@ -36,8 +36,14 @@ def test_initialisation_reproduces_reference(path):
     from importlib import import_module
     nets = import_module(load_pkg().__name__ + ".networks")
     z = np.load(path)
+    if "rtr_norms" in z.files:
+        pytest.skip("Q4 not-taken fixture: weights rescaled after the reference init")
     torch.manual_seed(int(z["seed"]))
-    m = nets.make_model(str(z["mode"]), [int(v) for v in z["layers"]], str(z["activation"]))
+    layers = [int(v) for v in z["layers"]]
+    if str(z["problem"]) == "heston":      # the reference builds on [D+1, ...] and replaces the input layers
+        m = nets.make_heston_model(str(z["mode"]), [2] + layers[1:], str(z["activation"]), layers[0])
+    else:
+        m = nets.make_model(str(z["mode"]), layers, str(z["activation"]))
     flat = torch.cat([p.reshape(-1) for p in m.state_dict().values()]).numpy()
     np.testing.assert_array_equal(flat, z["params"])
 
@@ -108,6 +114,38 @@ def test_correlation_matrix_recipe_matches_reference_fixture():
     np.testing.assert_allclose(obj.generate_correlation_matrix(4), z["corr"], rtol=0, atol=1e-12)
 
 
+def test_heston_spec_and_expressions():
+    """HestonFBSNN problem spec and torch expressions vs heston_dnnpde.py:546-609
+    (via the oracle's restatement, k = 1 and k = 3)."""
+    pkg = load_pkg()
+    for k, payoff in ((1, "discontinuous"), (3, "continuous")):
+        obj = object.__new__(pkg.HestonFBSNN)
+        obj.__dict__.update(n_assets=k, strike=1.0, kappa=2.0, theta=0.2, sigma=0.3, rho=0.8, v0=0.2,
+                            payoff_type=payoff, device=torch.device("cpu"))
+        spec = obj.problem_spec()
+        assert spec.kind == "heston" and spec.g_cols == k and spec.u_clamp and not spec.q3
+        assert spec.g == ("call_mean" if payoff == "discontinuous" else "smooth_call")
+        h = fr.Heston(k=k, payoff=payoff)
+        torch.manual_seed(k)
+        X = torch.rand(5, 2 * k) + 0.5
+        assert torch.allclose(obj.g_tf(X), h.g(X[:, :k]))
+        mu = obj.mu_tf(None, X)
+        assert torch.allclose(mu[:, :k], 0.05 * X[:, :k]) and torch.allclose(mu[:, k:], 2.0 * (0.2 - X[:, k:]))
+        full = obj._full_state(np.ones((1, k)))
+        assert full.shape == (1, 2 * k) and torch.all(full[0, k:] == 0.2)
+
+
+def test_optimizer_defaults_are_torch_defaults():
+    """OPT_DEFAULTS mirror optim.X(params, lr=lr) of torch (nd_BSPDE_case.py:331-350)."""
+    from importlib import import_module
+    fb = import_module(load_pkg().__name__ + ".fbsnn")
+    p = [torch.nn.Parameter(torch.zeros(2))]
+    for name, kw in fb.OPT_DEFAULTS.items():
+        d = getattr(torch.optim, name)(p, lr=1e-3).defaults
+        for k, v in kw.items():
+            assert d[k] == v, (name, k)
+
+
 def test_optimizer_names():
     pkg = load_pkg()
     obj = object.__new__(pkg.CallOption)
@@ -115,4 +153,5 @@ def test_optimizer_names():
         obj._check_optimizer("Nadam")
     with pytest.raises(NotImplementedError):
         obj._check_optimizer("LBFGS")
-    obj._check_optimizer("Adam")
+    for name in ("Adam", "SGD", "RMSprop", "AdamW", "Adadelta", "Adagrad", "Adamax", "ASGD"):
+        obj._check_optimizer(name)

@@ -20,6 +20,11 @@ def _load(p):
     return {k: z[k] for k in z.files}
 
 
+def _heston(g):
+    return dict(kappa=float(g["kappa"]), theta=float(g["theta"]), sigma=float(g["sigma"]), rho=float(g["rho"]),
+                v0=float(g["v0"]), payoff=str(g["payoff"]))
+
+
 @pytest.mark.parametrize("path", G1, ids=[os.path.basename(p)[3:-4] for p in G1])
 def test_restatement_matches_reference(path):
     """fp32 autograd restatement == reference run (same params, t, W)."""
@@ -27,11 +32,17 @@ def test_restatement_matches_reference(path):
     layers = [int(v) for v in g["layers"]]
     D, M = layers[0] - 1, int(g["M"])
     torch.set_num_threads(1)
-    model = fr.build_model(str(g["mode"]), layers, str(g["activation"]))
-    fr.set_flat_params(model, g["params"])
-    prob = fr.make_problem(str(g["problem"]), D)
-    res = fr.loss_and_grads(model, prob, torch.from_numpy(g["t"]), torch.from_numpy(g["W"]),
-                            torch.from_numpy(g["Xi"]), M, D)
+    if str(g["problem"]) == "heston":
+        model = fr.build_heston_model(str(g["mode"]), [2] + layers[1:], str(g["activation"]), D // 2)
+        fr.set_flat_params(model, g["params"])
+        res = fr.heston_loss_and_grads(model, fr.Heston(k=D // 2, **_heston(g)), torch.from_numpy(g["t"]),
+                                       torch.from_numpy(g["W"]), g["Xi"], M)
+    else:
+        model = fr.build_model(str(g["mode"]), layers, str(g["activation"]))
+        fr.set_flat_params(model, g["params"])
+        prob = fr.make_problem(str(g["problem"]), D)
+        res = fr.loss_and_grads(model, prob, torch.from_numpy(g["t"]), torch.from_numpy(g["W"]),
+                                torch.from_numpy(g["Xi"]), M, D)
     np.testing.assert_array_equal(res["X"], g["X"])          # the rollout is bit-exact
     np.testing.assert_allclose(res["loss"], g["loss"], rtol=1e-6)
     np.testing.assert_allclose(res["Y"], g["Y"], rtol=1e-6, atol=1e-6)
@@ -47,11 +58,13 @@ def test_timeparallel_matches_reference(path):
     reference's fp32 loss / Z / gradient to fp32 accuracy."""
     g = _load(path)
     layers = [int(v) for v in g["layers"]]
+    heston = str(g["problem"]) == "heston"
     out = tp.loss_grad(g["params"].astype(np.float64), str(g["mode"]), layers, str(g["activation"]),
                        str(g["problem"]), g["t"].astype(np.float64), g["W"].astype(np.float64),
-                       g["Xi"].astype(np.float64))
+                       (g["Xi_full"] if heston else g["Xi"]).astype(np.float64),
+                       heston=_heston(g) if heston else None)
     np.testing.assert_allclose(out["loss"], g["loss"], rtol=2e-5)
-    np.testing.assert_allclose(out["X"], g["X"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(out["X"], g["X"], rtol=1e-6, atol=1e-6 * max(1.0, np.abs(g["X"]).max()))
     np.testing.assert_allclose(out["Y"], g["Y"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(out["Z"], g["Z"], rtol=1e-4, atol=1e-5)
     used = g["used"]
@@ -66,6 +79,14 @@ def test_restated_training_matches_reference(path):
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
     torch.set_num_threads(1)
+    if str(g["problem"]) == "heston":
+        model = fr.build_heston_model(str(g["mode"]), [2] + layers[1:], str(g["activation"]), D // 2)
+        fr.set_flat_params(model, g["params0"])
+        np.random.seed(int(g["batch_seed"]))
+        fr.heston_train(model, fr.Heston(k=D // 2, **_heston(g)), g["Xi"], M, N, float(g["T"]), int(g["iters"]),
+                        float(g["lr"]), Mm=float(g["Mm"]))
+        np.testing.assert_allclose(fr.flat_params(model), g["params1"], rtol=0, atol=2e-6)
+        return
     model = fr.build_model(str(g["mode"]), layers, str(g["activation"]))
     fr.set_flat_params(model, g["params0"])
     prob = fr.make_problem(str(g["problem"]), D)
