@@ -118,23 +118,19 @@ __device__ __forceinline__ void zero(Mat<TT>& m) {
   for (int t = 0; t < TT; ++t) m.v[t] = floatx4{0.f, 0.f, 0.f, 0.f};
 }
 
-// residual of row r (n < N: Y_{n+1} - Ytilde_{n+1}, DeepBSDE.py:223-228;
-// n == N: Y_N - g(X_N), :232) and, for terminal rows, the grad-g scale
-__device__ __forceinline__ float row_residual(const CotanParams& p, int r, int n, float& gsc) {
-  const float* rs = p.rowsum + (size_t)r * 8;
-  const float y = p.u[r];
-  gsc = 0.f;
-  if (n < p.N1 - 1) {
-    const float dt = p.xin[(size_t)(r + 1) * p.Dp] - p.xin[(size_t)r * p.Dp];
-    const float zs = p.q3S ? rs[5] * p.q3S[n] : rs[0];
-    const float phi = p.phi_r * (y - p.phi_c * rs[1]) + p.phi_zz * rs[2];
-    return p.u[r + 1] - (y + phi * dt + zs);
-  }
-  return y - terminal_g(p.g_kind, rs[3], rs[4], p.gcols, p.strike, p.g_alpha, gsc);
+// residual of a non-terminal row from its row sums rs, Y = y, Y_next = yn,
+// dt and the Q3 sum: Y_{n+1} - Ytilde_{n+1} (DeepBSDE.py:223-228)
+__device__ __forceinline__ float step_residual(const CotanParams& p, floatx4 rs0, floatx4 rs1, float y, float yn,
+                                               float dt, float q3) {
+  const float zs = p.q3S ? rs1[1] * q3 : rs0[0];
+  const float phi = p.phi_r * (y - p.phi_c * rs0[1]) + p.phi_zz * rs0[2];
+  return yn - (y + phi * dt + zs);
 }
 
 // cotangents of row r: ubar (d loss / d Y_r) and the per-row scalars the zbar
 // entries need.  The loss of the row is res^2 + |Z - grad g|^2 (terminal).
+// Every load is issued up front from clamped indices (one memory latency, not
+// a chain of dependent ones).
 struct RowCotan {
   bool valid, term;
   int n;
@@ -143,24 +139,31 @@ struct RowCotan {
 __device__ __forceinline__ RowCotan row_cotan(const CotanParams& p, int r) {
   RowCotan c{};
   c.valid = r < p.R;
-  if (!c.valid) return c;
-  c.n = r % p.N1;
-  c.term = c.n == p.N1 - 1;
-  c.res = row_residual(p, r, c.n, c.gsc);
-  c.mask = p.rowsum[(size_t)r * 8 + 6];
-  if (c.term) {
+  const int rr = c.valid ? r : 0;
+  const int n = rr % p.N1;
+  const bool term = n == p.N1 - 1;
+  const int rn = term ? rr : rr + 1, rp = n >= 1 ? rr - 1 : rr;
+  const floatx4 a0 = *(const floatx4*)(p.rowsum + (size_t)rr * 8), a1 = *(const floatx4*)(p.rowsum + (size_t)rr * 8 + 4);
+  const floatx4 b0 = *(const floatx4*)(p.rowsum + (size_t)rp * 8), b1 = *(const floatx4*)(p.rowsum + (size_t)rp * 8 + 4);
+  const float y = p.u[rr], yn = p.u[rn], yp = p.u[rp];
+  const float t = p.xin[(size_t)rr * p.Dp], tn = p.xin[(size_t)rn * p.Dp], tp = p.xin[(size_t)rp * p.Dp];
+  const float q = p.q3S ? p.q3S[term ? 0 : n] : 0.f, qp = p.q3S ? p.q3S[n >= 1 ? n - 1 : 0] : 0.f;
+  c.n = n;
+  c.term = term;
+  c.mask = a1[2];
+  if (term) {
+    c.res = y - terminal_g(p.g_kind, a0[3], a1[0], p.gcols, p.strike, p.g_alpha, c.gsc);
     c.ub = 2.f * c.res;
   } else {
-    c.dt = p.xin[(size_t)(r + 1) * p.Dp] - p.xin[(size_t)r * p.Dp];
+    c.dt = tn - t;
+    c.res = step_residual(p, a0, a1, y, yn, c.dt, q);
     c.ub = -2.f * c.res * (1.f + p.phi_r * c.dt);
-    c.q3s = p.q3S ? p.q3S[c.n] : 0.f;
+    c.q3s = q;
   }
-  if (c.n >= 1) {
-    float g2;
-    c.ub += 2.f * row_residual(p, r - 1, c.n - 1, g2);
-  }
+  if (n >= 1) c.ub += 2.f * step_residual(p, b0, b1, yp, y, t - tp, qp);
   c.ub *= c.mask;
   c.coefY = -2.f * c.res;
+  if (!c.valid) c.res = c.ub = c.coefY = 0.f;   // padding rows carry no cotangent
   return c;
 }
 // zbar of column col (1 <= col <= D) from x, z, (sigma dW) of that column;

@@ -13,10 +13,30 @@
 // rank holding paths [path0, path0 + M) draws what one device would draw.
 // The device-mode time grid is the reference's: t_n = fp32(fp64 cumsum of
 // T/N) (DeepBSDE.py:250-258).
+//
+// HIP contracts a*b + c into an FMA by default (-ffp-contract=fast), and its
+// __fmul_rn/__fadd_rn are plain operators whose contract flag comes from the
+// header that defines them, so a pragma at the call site does not stop the
+// fusion.  The path kernels use rn_mul/rn_add/rn_sub below, whose operations
+// carry no contract flag: the reference (torch CPU) rounds each product and
+// sum, and X is bit-exact against it.
 #pragma once
 #include "philox.hpp"
 
 namespace dbsde {
+
+__device__ __forceinline__ float rn_mul(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float rn_add(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ float rn_sub(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
 
 enum PathOut { PATH_ROLLOUT = 0, PATH_FETCH_W = 1, PATH_FETCH_DW = 2 };
 
@@ -52,7 +72,7 @@ __device__ __forceinline__ void step_block(const RolloutArgs& p, int m, int d, i
       const int n = min(n0 + k + 1, p.N);
       const float w1 = p.W[((size_t)m * N1 + n) * p.nb + d];
       t1[k] = p.t[(size_t)m * N1 + n];
-      dw[k] = __fsub_rn(w1, w0);
+      dw[k] = rn_sub(w1, w0);
       w0 = w1;
     }
   } else {
@@ -123,11 +143,11 @@ __global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
         xr[0] = t0;
         xr[p.D + 1] = 1.0f;
       }
-      const float dt = __fsub_rn(t1[k], t0);
-      const float sg = __fadd_rn(__fmul_rn(p.sig_a, x), p.sig_b);
-      const float s = __fmul_rn(sg, dw[k]);
+      const float dt = rn_sub(t1[k], t0);
+      const float sg = rn_add(rn_mul(p.sig_a, x), p.sig_b);
+      const float s = rn_mul(sg, dw[k]);
       p.sdw[r * p.ldx + 1 + d] = s;
-      x = __fadd_rn(__fadd_rn(x, __fmul_rn(__fmul_rn(p.mu_a, x), dt)), s);
+      x = rn_add(rn_add(x, rn_mul(rn_mul(p.mu_a, x), dt)), s);
       t0 = t1[k];
       ++r;
     }
@@ -228,11 +248,11 @@ __global__ void __launch_bounds__(256) rollout_corr_kernel(RolloutArgs p) {
           xr[0] = t0;
           xr[p.D + 1] = 1.0f;
         }
-        const float dt = __fsub_rn(t1, t0);
-        const float sg = __fadd_rn(__fmul_rn(p.sig_a, x[i]), p.sig_b);
-        const float s = __fmul_rn(sg, acc[i]);
+        const float dt = rn_sub(t1, t0);
+        const float sg = rn_add(rn_mul(p.sig_a, x[i]), p.sig_b);
+        const float s = rn_mul(sg, acc[i]);
         p.sdw[r * p.ldx + 1 + d] = s;
-        x[i] = __fadd_rn(__fadd_rn(x[i], __fmul_rn(__fmul_rn(p.mu_a, x[i]), dt)), s);
+        x[i] = rn_add(rn_add(x[i], rn_mul(rn_mul(p.mu_a, x[i]), dt)), s);
       }
       t0 = t1;
     }
@@ -297,18 +317,18 @@ __global__ void __launch_bounds__(256) rollout_heston_kernel(RolloutArgs p) {
         xr[0] = t0;
         xr[p.D + 1] = 1.0f;
       }
-      const float dt = __fsub_rn(t1[kk], t0);
-      const float muS = clamp100(__fmul_rn(p.mu_a, S));
-      const float muV = clamp100(__fmul_rn(p.kappa, __fsub_rn(p.theta, v)));
-      const float sv = sqrtf(fmaxf(v, 1e-8f));
-      const float sigS = __fmul_rn(sv, S), sigV = __fmul_rn(p.hsig, sv);
+      const float dt = rn_sub(t1[kk], t0);
+      const float muS = clamp100(rn_mul(p.mu_a, S));
+      const float muV = clamp100(rn_mul(p.kappa, rn_sub(p.theta, v)));
+      const float sv = sqrtf(fmaxf(v, 1e-8f));   // correctly rounded (-fhip-fp32-correctly-rounded-divide-sqrt)
+      const float sigS = rn_mul(sv, S), sigV = rn_mul(p.hsig, sv);
       const float d00 = clamp100(sigS), d11 = clamp100(sigV);
-      const float d01 = clamp100(__fmul_rn(p.rho, sigV)), d10 = clamp100(__fmul_rn(p.rho, sigS));
+      const float d01 = clamp100(rn_mul(p.rho, sigV)), d10 = clamp100(rn_mul(p.rho, sigS));
       const float w = dw[kk];
-      p.sdw[r * p.ldx + 1 + i] = __fadd_rn(__fmul_rn(d00, w), __fmul_rn(d01, w));
-      p.sdw[r * p.ldx + 1 + k + i] = __fadd_rn(__fmul_rn(d10, w), __fmul_rn(d11, w));
-      S = __fadd_rn(__fadd_rn(S, __fmul_rn(muS, dt)), __fmul_rn(__fadd_rn(d00, d01), w));
-      v = __fadd_rn(__fadd_rn(v, __fmul_rn(muV, dt)), __fmul_rn(__fadd_rn(d10, d11), w));
+      p.sdw[r * p.ldx + 1 + i] = rn_add(rn_mul(d00, w), rn_mul(d01, w));
+      p.sdw[r * p.ldx + 1 + k + i] = rn_add(rn_mul(d10, w), rn_mul(d11, w));
+      S = rn_add(rn_add(S, rn_mul(muS, dt)), rn_mul(rn_add(d00, d01), w));
+      v = rn_add(rn_add(v, rn_mul(muV, dt)), rn_mul(rn_add(d10, d11), w));
       t0 = t1[kk];
       ++r;
     }

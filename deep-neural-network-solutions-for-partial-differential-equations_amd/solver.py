@@ -125,7 +125,7 @@ class NativeSolver:
         if Xi.numel() not in (D, M * D):
             raise ValueError("Xi must hold 1 or M rows of D values")
         self._check_tensor(t, "t", M * (N + 1))
-        self._check_tensor(W, "W", M * (N + 1) * D)
+        self._check_tensor(W, "W", M * (N + 1) * self.nb)
         self._check_tensor(loss, "loss", 1)
         self._check_tensor(X, "X", M * (N + 1) * D)
         self._check_tensor(Y, "Y", M * (N + 1))

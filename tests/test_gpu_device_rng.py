@@ -105,11 +105,9 @@ def test_correlated_device_mode(pkg, dev, D):
     """with_corr...py:339-341: dW = L (sqrt(dt) z), L staged in LDS (rollout_corr_kernel)."""
     rs = np.random.RandomState(D)
     A = rs.normal(size=(D, D))
-    C = A @ A.T
-    np.fill_diagonal(C, 1)
+    C = A @ A.T + D * np.eye(D)
     d = np.sqrt(np.diag(C))
-    C = C / np.outer(d, d) + 1e-3 * np.eye(D)
-    L = np.linalg.cholesky(C)
+    L = np.linalg.cholesky(C / np.outer(d, d))
     s = solver(pkg, dev, D, pkg.ProblemSpec(**BASKET), layers=[D + 1, 16, 16, 16, 16, 1])
     s.set_corr(L)
     M, N = 24, 10

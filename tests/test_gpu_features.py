@@ -129,8 +129,9 @@ def test_heston_predict_returns_S_v_Y(pkg, dev):
                         device=dev)
     m.params.copy_(torch.from_numpy(g["params"]).to(dev))
     S, v, Y = m.predict(g["Xi"], g["t"], g["W"])
-    np.testing.assert_array_equal(S.cpu().numpy(), g["X"][:, :, 0:1])
-    np.testing.assert_array_equal(v.cpu().numpy(), g["X"][:, :, 1:2])
+    # 1-ulp torch (MKL vsSqrt) near-tie differences propagate, see test_gpu_parity.py
+    np.testing.assert_allclose(S.cpu().numpy(), g["X"][:, :, 0:1], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(v.cpu().numpy(), g["X"][:, :, 1:2], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(Y.cpu().numpy(), g["Y"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Y"]).max()))
 
 
