@@ -66,6 +66,16 @@ struct dbsde_ctx {
   // (weight repack during the rollout, loss sum and grad clear during phase C)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
+  // path-chunked phase pipeline: chunk i runs phase A then phase C on stream
+  // pipe[i % 2], so one chunk's phase C fills the other's phase-A tail
+  hipStream_t pipe2 = nullptr;
+  hipStream_t pipe_more[2] = {nullptr, nullptr};   // streams 3 and 4 (DBSDE_PIPES=3|4)
+  int pipes = 2;
+  hipEvent_t ev_pipe[2] = {nullptr, nullptr};
+  hipEvent_t ev_more[2] = {nullptr, nullptr};
+  hipEvent_t ev_prof[2] = {nullptr, nullptr};
+  int chunks = 2;
+  int chunk0 = 0;
   bool side_pending[2] = {false, false};
 
   // ---- network description
@@ -93,8 +103,9 @@ struct dbsde_ctx {
   long long* d_woffs = nullptr;   // NAIS: W_j offsets in the flat params
   float** d_rtr = nullptr;
   float** d_abar = nullptr;
-  float** d_sbuf = nullptr;
   double* proj_part = nullptr;
+  double* dot_part = nullptr;     // <Abar_j, R_j> partials from the gradient finalize (one per 64 elements)
+  int dot_nblk = 0;
   unsigned char* d_used = nullptr;
   PackDesc* d_prep = nullptr;
   int n_prep = 0;
@@ -406,22 +417,21 @@ int build_buffers(dbsde_ctx* c) {
   const int LW = c->L[1];
   if (c->proj) {
     if ((rc = dalloc_t(c, &c->norms, (size_t)K + 1))) return rc;
-    std::vector<float*> hr(K), ha(K), hs(K);
+    std::vector<float*> hr(K), ha(K);
     std::vector<long long> hw(K);
     for (int j = 1; j <= K; ++j) {
       if ((rc = dalloc_t(c, &c->rtr[j], (size_t)LW * LW))) return rc;
       if ((rc = dalloc_t(c, &c->abar[j], (size_t)LW * LW))) return rc;
-      if ((rc = dalloc_t(c, &hs[j - 1], (size_t)LW * LW))) return rc;
       hr[j - 1] = c->rtr[j];
       ha[j - 1] = c->abar[j];
       hw[j - 1] = c->B[j - 1].w;
     }
     if ((rc = dalloc_t(c, &c->proj_part, (size_t)K * std::max((LW * LW + 255) / 256, ((LW + 15) / 16) * ((LW + 15) / 16)))))
       return rc;
+    c->dot_nblk = (LW * LW + 63) / 64;
+    if ((rc = dalloc_t(c, &c->dot_part, (size_t)K * c->dot_nblk))) return rc;
     if ((rc = dalloc_t(c, &c->d_rtr, K))) return rc;
     if ((rc = dalloc_t(c, &c->d_abar, K))) return rc;
-    if ((rc = dalloc_t(c, &c->d_sbuf, K))) return rc;
-    HIPC(c, hipMemcpy(c->d_sbuf, hs.data(), K * sizeof(float*), hipMemcpyHostToDevice));
     if ((rc = dalloc_t(c, &c->d_woffs, K))) return rc;
     HIPC(c, hipMemcpy(c->d_rtr, hr.data(), K * sizeof(float*), hipMemcpyHostToDevice));
     HIPC(c, hipMemcpy(c->d_abar, ha.data(), K * sizeof(float*), hipMemcpyHostToDevice));
@@ -479,11 +489,16 @@ int build_buffers(dbsde_ctx* c) {
   for (int j = 1; j <= K; ++j) {
     const Lin& b = c->B[j - 1];
     if (c->proj) {
+      const int nblk = ((LW + 15) / 16) * ((LW + 15) / 16);
       PackDesc d = mk_desc(c->rtr[j], LW, c->Bf[j], c->Wp[j - 1], LW, LW, 0, PK_NEGPROJ);
-      d.proj = c->norms + (j - 1);
+      d.proj = c->proj_part + (size_t)(j - 1) * nblk;
+      d.proj_n = nblk;
+      d.proj_norm = c->norms + (j - 1);
       P.push_back(frag(d, c->imgF[j], TW, TW, 0, 0));
       d = mk_desc(c->rtr[j], LW, c->Bb[j], c->Wp[j], LW, LW, 1, PK_NEGPROJ);
-      d.proj = c->norms + (j - 1);
+      d.proj = c->proj_part + (size_t)(j - 1) * nblk;
+      d.proj_n = nblk;
+      d.proj_norm = nullptr;
       P.push_back(frag(d, c->imgB[j], TW, TW, 0, 0));
     } else {
       P.push_back(frag(mk_desc(ptag(b.w), b.in, c->Bf[j], c->Wp[j - 1], b.out, b.in, 0, PK_COPY), c->imgF[j], TW,
@@ -527,6 +542,8 @@ int build_buffers(dbsde_ctx* c) {
       wsum(j, 0, D + 1, v.out, 1, gtag(c->B[j - 1].b), 1, 1.f);
       const Lin& b = c->B[j - 1];
       wsum(K + j, 0, 0, b.out, b.in, c->abar[j], LW, -1.f);  // Abar = -Bbar
+      F.back().dotR = c->rtr[j];
+      F.back().dot_part = c->dot_part + (size_t)(j - 1) * c->dot_nblk;
     }
     // output layer: row 0 of problem 2K+1 is w_out, element (1, 0) is b_out
     wsum(2 * K + 1, 0, 0, 1, c->out.in, gtag(c->out.w), 1, 1.f);
@@ -574,6 +591,8 @@ int build_buffers(dbsde_ctx* c) {
       const Lin& b = c->B[j - 1];
       if (c->proj) {
         slabsum(j, 0, 0, b.out, b.in, c->abar[j], LW, -1.f);  // Abar = -Bbar
+        F.back().dotR = c->rtr[j];
+        F.back().dot_part = c->dot_part + (size_t)(j - 1) * c->dot_nblk;
       } else {
         slabsum(j, 0, 0, b.out, b.in, gtag(b.w), b.in, 1.f);
         slabsum(j, 0, c->Wp[j - 1], b.out, 1, gtag(b.b), 1, 1.f);
@@ -759,6 +778,22 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
   d.src2 = untag(d.src2, params, grad);
   d.dst = (float*)untag(d.dst, params, grad);
   const int total = d.rows * d.cols;
+  // NAIS projection: |RtR|_F from rtr_params_kernel's partials (fixed order)
+  __shared__ float nrm_s;
+  if (d.mode == PK_NEGPROJ) {
+    if (threadIdx.x < 64) {   // wave 0: lane b holds partials b, b + 64, ... ; fixed-order butterfly
+      double sq = 0.0;
+      for (int b = threadIdx.x; b < d.proj_n; b += 64) sq += d.proj[b];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+      if (threadIdx.x == 0) {
+        const double n = sqrt(sq);
+        nrm_s = (float)n;
+        if (blockIdx.x == 0 && d.proj_norm) *d.proj_norm = n;
+      }
+    }
+    __syncthreads();
+  }
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int r = i / d.cols, cc = i - r * d.cols;
     float v;
@@ -768,7 +803,7 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
       v = d.src[(size_t)r * d.src_ld + cc] + d.src2[(size_t)r * d.src2_ld + cc];
     } else if (d.mode == PK_NEGPROJ) {
       const float rv = d.src[(size_t)r * d.src_ld + cc];
-      const float nrm = (float)d.proj[0];
+      const float nrm = nrm_s;
       float a = rv;
       if (nrm > 0.98f) a = ((float)0.98994949366116658 * rv) / sqrtf(nrm);
       a = a + (r == cc ? 0.01f : 0.f);
@@ -845,57 +880,54 @@ __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, co
   }
   if (threadIdx.x == 0) part[j * nblk + blockIdx.x] = red[0];
 }
-// norms[j] = sqrt(sum of partials) ; thread j (deterministic order)
-__global__ void norm_from_parts_kernel(const double* part, int nblk, int K, double* norms) {
-  const int j = threadIdx.x;
-  if (j >= K) return;
-  double s = 0.0;
-  for (int b = 0; b < nblk; ++b) s += part[j * nblk + b];
-  norms[j] = sqrt(s);
-}
-// <Abar_j, R_j> partial sums per block
-__global__ void __launch_bounds__(256) proj_dot_kernel(float* const* abar, float* const* rtr, int L, double* part,
-                                                       int nblk) {
-  const int j = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  double d = 0.0;
-  if (i < L * L) d = (double)abar[j][i] * (double)rtr[j][i];
-  __shared__ double red[256];
-  red[threadIdx.x] = d;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
+// NAIS projection adjoint (Functions/naisnet.py:30-39 reversed), one kernel:
+//   Abar_j = dL/dA_j (slab sums), R_j = W_j^T W_j, n = |R_j|_F
+//   Rbar   = c n^-1/2 (Abar - 1/2 <Abar, R> R / n^2)  (Q4 branch taken, c = sqrt 0.98)
+//          = Abar                                     (not taken)
+//   Wbar_j = W_j (Rbar + Rbar^T)  -> grad
+// Every block recomputes <Abar_j, R_j> in the same fixed order (L^2 products,
+// cheap), so no separate reduction launch is needed; S = Rbar + Rbar^T is
+// formed on the fly in the B tile of the LDS-tiled GEMM.
+__global__ void __launch_bounds__(256) proj_backward_kernel(const float* params, const long long* woffs,
+                                                            float* const* abar, float* const* rtr, int L,
+                                                            const double* norms, const double* dot_part, int dot_nblk,
+                                                            float* grad) {
+  __shared__ float As[16][17], Bs[16][17];
+  __shared__ double dot_s;
+  const int j = blockIdx.y, nt = (L + 15) / 16;
+  const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
+  const float* Ab = abar[j];
+  const float* R = rtr[j];
+  if (threadIdx.x < 64) {   // <Abar_j, R_j> from the finalize partials, fixed-order butterfly
+    double dsum = 0.0;
+    for (int b = threadIdx.x; b < dot_nblk; b += 64) dsum += dot_part[(size_t)j * dot_nblk + b];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o);
+    if (threadIdx.x == 0) dot_s = dsum;
   }
-  if (threadIdx.x == 0) part[j * nblk + blockIdx.x] = red[0];
-}
-// S = Rbar + Rbar^T with Rbar = c n^-1/2 (Abar - 1/2 <Abar,R> R / n^2) if the
-// Q4 branch was taken, else Abar.  Written over abar's scratch twin sbuf.
-__global__ void __launch_bounds__(256) proj_s_kernel(float* const* abar, float* const* rtr, float* const* sbuf, int L,
-                                                     const double* part, int nblk, const double* norms) {
-  const int j = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= L * L) return;
-  double dot = 0.0;
-  for (int b = 0; b < nblk; ++b) dot += part[j * nblk + b];
+  __syncthreads();
+  const double dot = dot_s;
   const double n = norms[j];
   const bool taken = (float)n > 0.98f;
   const float cA = taken ? (float)(0.98994949366116658 / sqrt(n)) : 1.f;
   const float cR = taken ? (float)(0.98994949366116658 / sqrt(n) * 0.5 * dot / (n * n)) : 0.f;
-  const int a = i / L, b = i - a * L;
-  const float* Ab = abar[j];
-  const float* R = rtr[j];
-  sbuf[j][i] = cA * (Ab[a * L + b] + Ab[b * L + a]) - cR * (R[a * L + b] + R[b * L + a]);
-}
-// Wbar_j = W_j S_j  -> grad
-__global__ void __launch_bounds__(256) proj_wbar_kernel(const float* params, const long long* woffs,
-                                                        float* const* sbuf, int L, float* grad) {
-  __shared__ float As[16][17], Bs[16][17];
-  const int j = blockIdx.y, nt = (L + 15) / 16;
-  const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
-  const float v = tile_gemm16<false>(params + woffs[j], sbuf[j], L, ti, tj, As, Bs);
-  const int row = ti * 16 + (threadIdx.x >> 4), col = tj * 16 + (threadIdx.x & 15);
-  if (row < L && col < L) grad[woffs[j] + row * L + col] = v;
+  const float* W = params + woffs[j];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int row = ti * 16 + ty, col = tj * 16 + tx;
+  float acc = 0.f;
+  for (int k0 = 0; k0 < L; k0 += 16) {
+    const int kr = k0 + tx, kc = k0 + ty;
+    As[ty][tx] = (row < L && kr < L) ? W[row * L + kr] : 0.f;
+    float sv = 0.f;
+    if (kc < L && col < L)
+      sv = cA * (Ab[kc * L + col] + Ab[col * L + kc]) - cR * (R[kc * L + col] + R[col * L + kc]);
+    Bs[ty][tx] = sv;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += As[ty][k] * Bs[k][tx];
+    __syncthreads();
+  }
+  if (row < L && col < L) grad[woffs[j] + row * L + col] = acc;
 }
 }  // namespace dbsde
 
@@ -909,7 +941,6 @@ int prep_weights(dbsde_ctx* c, const float* params) {
     const int nblk = ((LW + 15) / 16) * ((LW + 15) / 16);
     RUN(c, "rtr", fl, 0.0,
         rtr_params_kernel<<<dim3(nblk, c->K), 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, c->proj_part, nblk));
-    RUN(c, "rtr_norm", 0.0, 0.0, norm_from_parts_kernel<<<1, 64, 0, s>>>(c->proj_part, nblk, c->K, c->norms));
   }
   RUN(c, "pack_weights", 0.0, 0.0, pack_tagged_kernel<<<dim3(8, c->n_prep), 256, 0, s>>>(c->d_prep, params, nullptr));
   return DBSDE_OK;
@@ -970,14 +1001,10 @@ int finalize_grads(dbsde_ctx* c, const float* params, float* grad) {
   RUN(c, "grad_finalize", 0.0, 0.0, slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad));
   if (c->proj) {
     const int LW = c->L[1];
-    const int nblk = (LW * LW + 255) / 256;
-    const dim3 g(nblk, c->K);
-    RUN(c, "proj_dot", 0.0, 0.0, proj_dot_kernel<<<g, 256, 0, s>>>(c->d_abar, c->d_rtr, LW, c->proj_part, nblk));
-    RUN(c, "proj_s", 0.0, 0.0,
-        proj_s_kernel<<<g, 256, 0, s>>>(c->d_abar, c->d_rtr, c->d_sbuf, LW, c->proj_part, nblk, c->norms));
     const int ntile = ((LW + 15) / 16) * ((LW + 15) / 16);
-    RUN(c, "proj_wbar", 2.0 * c->K * LW * (double)LW * LW, 0.0,
-        proj_wbar_kernel<<<dim3(ntile, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_sbuf, LW, grad));
+    RUN(c, "proj_backward", 2.0 * c->K * LW * (double)LW * LW, 0.0,
+        proj_backward_kernel<<<dim3(ntile, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_abar, c->d_rtr, LW, c->norms,
+                                                               c->dot_part, c->dot_nblk, grad));
   }
   return DBSDE_OK;
 }
@@ -1217,10 +1244,20 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
   if (!rc) rc = build_buffers(c);
   if (!rc) {
     hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->pipe2, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+      e = hipStreamCreateWithFlags(&c->pipe_more[i], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_more[i], hipEventDisableTiming);
+    }
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
       e = hipEventCreateWithFlags(&c->ev_fork[i], hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreate(&c->ev_prof[i]);
     }
+    if (const char* ch = getenv("DBSDE_CHUNKS")) c->chunks = std::max(1, std::min(16, atoi(ch)));
+    if (const char* ch = getenv("DBSDE_CHUNK0")) c->chunk0 = atoi(ch);
+    if (const char* ch = getenv("DBSDE_PIPES")) c->pipes = std::max(2, std::min(4, atoi(ch)));
     if (e != hipSuccess) rc = fail(c, DBSDE_EHIP, std::string("side stream: ") + hipGetErrorString(e));
   }
   if (rc) {
@@ -1237,11 +1274,19 @@ void dbsde_destroy(dbsde_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->side) (void)hipStreamSynchronize(c->side);
+  if (c->pipe2) (void)hipStreamSynchronize(c->pipe2);
   for (int i = 0; i < 2; ++i) {
     if (c->ev_fork[i]) (void)hipEventDestroy(c->ev_fork[i]);
     if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
+    if (c->ev_pipe[i]) (void)hipEventDestroy(c->ev_pipe[i]);
+    if (c->ev_prof[i]) (void)hipEventDestroy(c->ev_prof[i]);
   }
   if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->pipe2) (void)hipStreamDestroy(c->pipe2);
+  for (int i = 0; i < 2; ++i) {
+    if (c->pipe_more[i]) (void)hipStreamDestroy(c->pipe_more[i]);
+    if (c->ev_more[i]) (void)hipEventDestroy(c->ev_more[i]);
+  }
   for (auto& r : c->pending) {
     c->ev_pool.push_back(r.e0);
     c->ev_pool.push_back(r.e1);
@@ -1301,11 +1346,61 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     const int nv = nv_x(c);
     const double flA = 2.0 * R * ((D + 1.0) * nv + 2.0 * K * L[1] * (double)L[1] + (double)nv * D);
     const double byA = 4.0 * R * (c->Dp + 4.0 * S + 8.0);
-    RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+    const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
+    const double byC = 4.0 * R * (4.0 * c->Dp + 5.0 * S);
+    // chunks of whole paths and whole 64-row tiles (64 paths = 64 (N+1) rows)
+    int nch = grad ? c->chunks : 1;
+    while (nch > 1 && (M % 64 != 0 || (M / 64) % nch != 0)) --nch;
+    if (nch <= 1) {
+      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+    } else {
+      // phase A / phase C of chunk i on stream (i even ? main : pipe2); the
+      // two phases are timed as one pipelined segment
+      // chunk sizes in units of 64 paths; DBSDE_CHUNK0 sets the first chunk's
+      // units (the rest split evenly), else all chunks are equal
+      const int units = M / 64, utile = N1;   // 64 paths = N1 tiles of 64 rows
+      std::vector<int> cu(nch, units / nch);
+      if (c->chunk0 > 0 && c->chunk0 < units && nch == 2) {
+        cu[0] = c->chunk0;
+        cu[1] = units - c->chunk0;
+      }
+      if (c->prof) HIPC(c, hipEventRecord(c->ev_prof[0], s));
+      HIPC(c, hipEventRecord(c->ev_pipe[0], s));
+      const int np = std::min(c->pipes, nch);
+      hipStream_t ps[4] = {s, c->pipe2, c->pipe_more[0], c->pipe_more[1]};
+      for (int i = 1; i < np; ++i) HIPC(c, hipStreamWaitEvent(ps[i], c->ev_pipe[0], 0));
+      int t0 = 0;
+      for (int i = 0; i < nch; ++i) {
+        hipStream_t st = ps[i % np];
+        FusedArgs fc = fa;
+        fc.tile0 = t0;
+        const int tiles = cu[i] * utile;
+        kFused[fv].A<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
+        kFused[fv].C<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
+        t0 += tiles;
+      }
+      HIPC(c, hipGetLastError());
+      HIPC(c, hipEventRecord(c->ev_pipe[1], c->pipe2));
+      HIPC(c, hipStreamWaitEvent(s, c->ev_pipe[1], 0));
+      for (int i = 2; i < np; ++i) {
+        HIPC(c, hipEventRecord(c->ev_more[i - 2], ps[i]));
+        HIPC(c, hipStreamWaitEvent(s, c->ev_more[i - 2], 0));
+      }
+      if (c->prof) {
+        HIPC(c, hipEventRecord(c->ev_prof[1], s));
+        HIPC(c, hipEventSynchronize(c->ev_prof[1]));
+        float ms = 0.f;
+        HIPC(c, hipEventElapsedTime(&ms, c->ev_prof[0], c->ev_prof[1]));
+        ProfAgg& ag = c->agg[prof_id(c, "fused_phases_pipelined")];
+        ag.ms += ms;
+        ag.flops += flA + flC;
+        ag.bytes += byA + byC;
+        ag.n += 1;
+      }
+    }
     if (grad) {
-      const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
-      const double byC = 4.0 * R * (4.0 * c->Dp + 5.0 * S);
-      RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+      if (nch <= 1)
+        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
       nloss_parts = Rp / P3_ROWS;
     } else {
       RUN(c, "loss_rows", 0.0, 4.0 * R * 3.0 * D,

@@ -25,6 +25,7 @@ struct CotanParams {
 struct FusedArgs {
   int R, N1, D, Dp, W, S;   // rows, N+1, D, padded D, padded level width, level stride
   int has_v, act;
+  int tile0;                // first 64-row tile of this launch (path-chunked pipeline)
   int gcols;                // leading state columns entering g (row sums s_x, s_xx)
   int u_clamp;              // u = max(net, 0) (heston_dnnpde.py:568)
   float rho;

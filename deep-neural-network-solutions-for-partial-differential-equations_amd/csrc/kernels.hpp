@@ -609,7 +609,11 @@ struct PackDesc {
   float scale;         // PK_COPY / PK_SLABSUM / PK_ADD2 multiplier
   int nslab;           // PK_SLABSUM: slabs of stride slab_stride
   long long slab_stride;
-  const double* proj;  // PK_NEGPROJ: [norm, ...] of this block
+  const double* proj;  // PK_NEGPROJ: the |R_j|^2 partial sums of this block (rtr_params_kernel)
+  int proj_n;          //   number of partials
+  double* proj_norm;   //   |R_j|_F written here by block 0 (for the backward)
+  const float* dotR;   // PK_SLABSUM into Abar_j: R_j (same layout as dst); the block's
+  double* dot_part;    //   partial <Abar_j, R_j> goes to dot_part[blockIdx.x]
   // optional second destination: an MFMA fragment image (phase.hpp) of the
   // logical [out][in] matrix, element (dr + frow0, dc + fcol0) with
   // (dr, dc) = transpose ? (c, r) : (r, c); ftin = 16-col input blocks
@@ -801,14 +805,23 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
   __shared__ double part[4][64];
   part[grp][lane] = s;
   __syncthreads();
-  if (grp == 0 && e < total) {
-    const float v = d.scale * (float)((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
-    uintptr_t dv = (uintptr_t)d.dst;
-    float* dst = (dv & ((uintptr_t)1 << 61)) ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
-    if (d.transpose)
-      dst[(size_t)cc * d.dst_ld + r] = v;
-    else
-      dst[(size_t)r * d.dst_ld + cc] = v;
+  if (grp == 0) {
+    double dp = 0.0;
+    if (e < total) {
+      const float v = d.scale * (float)((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
+      uintptr_t dv = (uintptr_t)d.dst;
+      float* dst = (dv & ((uintptr_t)1 << 61)) ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
+      if (d.transpose)
+        dst[(size_t)cc * d.dst_ld + r] = v;
+      else
+        dst[(size_t)r * d.dst_ld + cc] = v;
+      if (d.dotR) dp = (double)v * (double)d.dotR[(size_t)r * d.dst_ld + cc];
+    }
+    if (d.dotR) {   // fixed-order wave reduction of the block's <Abar, R> partial
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
+      if (lane == 0) d.dot_part[blockIdx.x] = dp;
+    }
   }
 }
 

@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   __shared__ floatx4 wl[2 * BUF];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int row0 = blockIdx.x * P3_ROWS + wave * 16;
+  const int tile = blockIdx.x + p.tile0;   // 64-row tile (chunked launches offset it)
+  const int row0 = tile * P3_ROWS + wave * 16;
   const int S = p.S, Wd = p.W;
   PieceStager sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
   piece_dma(p.simgA[0], p.snfA[0], wl, wave, lane);
@@ -290,7 +291,8 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   __shared__ double lsum[P3_WAVES];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int row0 = blockIdx.x * P3_ROWS + wave * 16;
+  const int tile = blockIdx.x + p.tile0;   // 64-row tile (chunked launches offset it)
+  const int row0 = tile * P3_ROWS + wave * 16;
   const int S = p.S, Wd = p.W;
   PieceStager sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
   piece_dma(p.simgC[0], p.snfC[0], wl, wave, lane);
@@ -336,7 +338,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   zero(ad[0]);
   stage_mm<T, TD>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
     bload(av, p.Abuf, S, row0, 0);
-    if (threadIdx.x == 0) p.loss_part[blockIdx.x] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
+    if (threadIdx.x == 0) p.loss_part[tile] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
   });
 #pragma unroll
   for (int o = 0; o < T; ++o)
