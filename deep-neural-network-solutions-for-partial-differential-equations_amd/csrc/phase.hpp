@@ -53,12 +53,58 @@ __device__ __forceinline__ void bstore(const Mat<TT>& m, float* base, int ld, in
 #pragma unroll
   for (int t = 0; t < TT; ++t) *(floatx4*)(p + 16 * t) = m.v[t];
 }
+// Abuf and G live only between phase A and phase C, so they use the register
+// tile's own order: the 16 x 16 block at (row0, col0) is 256 contiguous floats
+// (lane-major), one 1 KB contiguous access per instruction instead of 16
+// 64-byte row pieces.  Needs row0, col0, ld multiples of 16.
+template <int TT>
+__device__ __forceinline__ void fstore(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
+  const int lane = threadIdx.x & 63;
+  float* p = base + (size_t)row0 * ld + col0 * 16 + 4 * lane;
+#pragma unroll
+  for (int t = 0; t < TT; ++t) *(floatx4*)(p + 256 * t) = m.v[t];
+}
+template <int TT>
+__device__ __forceinline__ void fload(Mat<TT>& m, const float* base, int ld, int row0, int col0) {
+  const int lane = threadIdx.x & 63;
+  const float* p = base + (size_t)row0 * ld + col0 * 16 + 4 * lane;
+#pragma unroll
+  for (int t = 0; t < TT; ++t) m.v[t] = *(const floatx4*)(p + 256 * t);
+}
+
+// streaming store for the arrays only the weight-gradient kernel reads, after
+// both phases (H, Delta, Hdot, Alpha, zbar): no L2 allocate, so Abuf / G / zfull,
+// which phase C re-reads shortly after phase A wrote them, keep the cache
+// (measured -13 us on the two phases, profiles/r2_ab_ntstore.txt)
+template <int TT>
+__device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
+  const int lane = threadIdx.x & 63;
+  float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);
+#pragma unroll
+  for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 16 * t));
+}
 
 __device__ __forceinline__ void glds16(const float* g, floatx4* l) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
-__device__ __forceinline__ void vm_wait0() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0)
+// s_waitcnt vmcnt(N) (expcnt / lgkmcnt untouched): vector-memory operations
+// complete in issue order, so this waits for everything but the N youngest
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
+// workgroup barrier WITHOUT __syncthreads()'s release fence: that fence emits
+// vmcnt(0), draining every store / load still in flight (the counted waits
+// above would be lost).  lgkmcnt(0) first: this wave's LDS reads of the
+// buffer the next DMA overwrites, and its LDS writes, are complete.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt / expcnt untouched
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // acc[o] += sum_{t in [T0, T1)} W(o, t) . b(t); img = the piece holding
 // fragment (o, t) at ((t - T0) * TO + o).  Output blocks in groups of OG
@@ -87,16 +133,22 @@ __device__ __forceinline__ void piece_dma(const float* img, int nf, floatx4* buf
   for (int f = wave; f < nf; f += P3_WAVES) glds16(img + (size_t)f * 256 + lane * 4, buf + f * 64);
 }
 
-// piece sequencer: wait for this piece, publish it, start the next one
+// piece sequencer: wait for this piece, publish it, start the next one.
+// NYOUNG = vector-memory operations this wave is guaranteed to have issued
+// after the piece's DMA (deferred stores, early loads): they may stay in flight
+// across the barrier.  Under-counting is safe, over-counting is a race.
 struct PieceStager {
   floatx4* wl;
   const float* const* img;
   const int* nf;
   int n, st, wave, lane, buf;
+  template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
-    vm_wait0();
-    __syncthreads();
+    vm_wait<NYOUNG>();
+    lds_barrier();
     if (st + 1 < n) piece_dma(img[st + 1], nf[st + 1], wl + ((st + 1) & 1) * buf, wave, lane);
+    // nothing issued later may be hoisted above the DMA (the NYOUNG counts)
+    __builtin_amdgcn_sched_barrier(0);
     const floatx4* cur = wl + (st & 1) * buf;
     ++st;
     return cur;
@@ -108,15 +160,20 @@ struct NoOp {
 };
 
 // one stage = one operand image: two pieces (one when TI == 1); `after` runs
-// right after the first piece's barrier (deferred stores, early loads)
-template <int TO, int TI, class F>
+// right after the first piece's barrier (deferred stores, early loads).
+// NPRE = vector-memory ops issued since the first piece's DMA (the previous
+// stage's epilogue), NAFTER = the ops `after` issues (both lower bounds).
+template <int TO, int TI, int NPRE, int NAFTER, class F>
 __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceStager& sg, int lane, F&& after) {
   constexpr int H = (TI + 1) / 2;
-  const floatx4* w = sg.next();
+  const floatx4* w = sg.template next<NPRE>();
   after();
+  // keep the deferred stores / early loads here: left to itself the scheduler
+  // sinks them to the end of the piece, right in front of the next vmcnt(0)
+  __builtin_amdgcn_sched_barrier(0);
   sgemm_piece<TO, TI, 0, H>(acc, b, w, lane);
   if constexpr (H < TI) {
-    w = sg.next();
+    w = sg.template next<NAFTER>();
     sgemm_piece<TO, TI, H, TI>(acc, b, w, lane);
   }
 }
@@ -142,8 +199,8 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   Mat<T> s1[K + 1];   // act'(a_j)
   Mat<T> h, acc;
   zero(acc);
-  stage_mm<T, TD>(acc, x, sg, lane, NoOp{});
-  bstore(acc, p.Abuf, S, row0, 0);
+  stage_mm<T, TD, TD, 0>(acc, x, sg, lane, NoOp{});
+  fstore(acc, p.Abuf, S, row0, 0);
 #pragma unroll
   for (int o = 0; o < T; ++o)
 #pragma unroll
@@ -156,15 +213,15 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero(acc);
-    stage_mm<T, T>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore(h, p.H, S, row0, (j - 1) * Wd); });
-    if (p.has_v) stage_mm<T, TD>(acc, x, sg, lane, NoOp{});
+    stage_mm<T, T, T, T>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd); });
+    if (p.has_v) stage_mm<T, TD, 0, 0>(acc, x, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o) {
       const floatx4 bb = p.has_v ? floatx4{0.f, 0.f, 0.f, 0.f} : *(const floatx4*)(p.beta[j - 1] + 16 * o + 4 * q);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc.v[o][r] += bb[r];
     }
-    bstore(acc, p.Abuf, S, row0, j * Wd);
+    fstore(acc, p.Abuf, S, row0, j * Wd);
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
@@ -195,7 +252,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
     }
     if (q == 0) p.u[row0 + cl] = uv;
   }
-  bstore(h, p.H, S, row0, K * Wd);
+  bstore_stream(h, p.H, S, row0, K * Wd);
   // input gradient: g_{K+1} = w_out, delta_K = w_out act'(a_K)
   Mat<T> g, dl;
 #pragma unroll
@@ -212,16 +269,17 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   SFor<0, K>::run([&](auto ic) __attribute__((always_inline)) {
     constexpr int j = K - decltype(ic)::value;
     auto prev = [&]() __attribute__((always_inline)) {   // (g_j, delta_j) of the previous step
-      if constexpr (j < K) bstore(g, p.G, S, row0, j * Wd);
-      bstore(dl, p.Delta, S, row0, j * Wd);
+      if constexpr (j < K) fstore(g, p.G, S, row0, j * Wd);
+      bstore_stream(dl, p.Delta, S, row0, j * Wd);
     };
     Mat<T> gn;
     zero(gn);
+    constexpr int NPREV = j < K ? 2 * T : T;
     if (p.has_v) {
-      stage_mm<TD, T>(z, dl, sg, lane, prev);      // Z += delta_j V_j
-      stage_mm<T, T>(gn, dl, sg, lane, NoOp{});    // delta_j B_j
+      stage_mm<TD, T, 0, NPREV>(z, dl, sg, lane, prev);   // Z += delta_j V_j
+      stage_mm<T, T, 0, 0>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
     } else {
-      stage_mm<T, T>(gn, dl, sg, lane, prev);
+      stage_mm<T, T, 0, NPREV>(gn, dl, sg, lane, prev);
     }
 #pragma unroll
     for (int o = 0; o < T; ++o)
@@ -232,9 +290,9 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
         dl.v[o][r] = gv * s1[j - 1].v[o][r];
       }
   });
-  stage_mm<TD, T>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
-    bstore(g, p.G, S, row0, 0);
-    bstore(dl, p.Delta, S, row0, 0);
+  stage_mm<TD, T, 0, 2 * T + TD>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
+    fstore(g, p.G, S, row0, 0);
+    bstore_stream(dl, p.Delta, S, row0, 0);
     bload(x, p.xin, p.Dp, row0, 0);
   });
   if (p.u_clamp) {
@@ -305,20 +363,27 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   Mat<TD> zb;
   float tz = 0.f;
   {
+    // all 3 TD row loads in flight at once (the branchy zbar formula would
+    // otherwise split them into TD dependent memory round trips)
     const size_t off = (size_t)r * p.Dp + 4 * q;
+    Mat<TD> xv, zv, sv;
 #pragma unroll
     for (int o = 0; o < TD; ++o) {
-      const floatx4 xv = *(const floatx4*)(cp.xin + off + 16 * o);
-      const floatx4 zv = *(const floatx4*)(cp.zfull + off + 16 * o);
-      const floatx4 sv = *(const floatx4*)(cp.sdw + off + 16 * o);
+      xv.v[o] = *(const floatx4*)(cp.xin + off + 16 * o);
+      zv.v[o] = *(const floatx4*)(cp.zfull + off + 16 * o);
+      sv.v[o] = *(const floatx4*)(cp.sdw + off + 16 * o);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int o = 0; o < TD; ++o)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int c = 16 * o + 4 * q + rr;
-        zb.v[o][rr] = (rc.valid && c >= 1 && c <= p.D) ? col_zbar(cp, rc, c, xv[rr], zv[rr], sv[rr], tz) : 0.f;
+        zb.v[o][rr] = (rc.valid && c >= 1 && c <= p.D) ? col_zbar(cp, rc, c, xv.v[o][rr], zv.v[o][rr], sv.v[o][rr], tz)
+                                                       : 0.f;
       }
-    }
   }
-  bstore(zb, p.zbar, p.Dp, row0, 0);
+  bstore_stream(zb, p.zbar, p.Dp, row0, 0);
   tz += __shfl_xor(tz, 16);
   tz += __shfl_xor(tz, 32);
   {
@@ -336,8 +401,8 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   Mat<T> ad[K + 1];   // adot_j
   Mat<T> hd, av;
   zero(ad[0]);
-  stage_mm<T, TD>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
-    bload(av, p.Abuf, S, row0, 0);
+  stage_mm<T, TD, TD, T>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
+    fload(av, p.Abuf, S, row0, 0);
     if (threadIdx.x == 0) p.loss_part[tile] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
   });
 #pragma unroll
@@ -347,17 +412,17 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero(ad[j]);
-    stage_mm<T, T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
-      bstore(hd, p.Hdot, S, row0, (j - 1) * Wd);
-      bload(av, p.Abuf, S, row0, j * Wd);
+    stage_mm<T, T, 0, 2 * T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
+      bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd);
+      fload(av, p.Abuf, S, row0, j * Wd);
     });
-    if (p.has_v) stage_mm<T, TD>(ad[j], zb, sg, lane, NoOp{});
+    if (p.has_v) stage_mm<T, TD, 0, 0>(ad[j], zb, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) hd.v[o][rr] = act_1<ACT>(av.v[o][rr]) * ad[j].v[o][rr] + p.rho * hd.v[o][rr];
   });
-  bstore(hd, p.Hdot, S, row0, K * Wd);
+  bstore_stream(hd, p.Hdot, S, row0, K * Wd);
   // reverse: p_{K+1} = ubar w_out ; alpha_K = w_out (ubar act'(a_K) + adot_K act''(a_K))
   Mat<T> pv, al;
   {
@@ -378,10 +443,10 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
     constexpr int j = K - decltype(ic)::value;
     Mat<T> acc, gg;
     zero(acc);
-    stage_mm<T, T>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
-      bstore(al, p.Alpha, S, row0, j * Wd);
-      bload(av, p.Abuf, S, row0, (j - 1) * Wd);
-      bload(gg, p.G, S, row0, (j - 1) * Wd);
+    stage_mm<T, T, 0, 3 * T>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
+      bstore_stream(al, p.Alpha, S, row0, j * Wd);
+      fload(av, p.Abuf, S, row0, (j - 1) * Wd);
+      fload(gg, p.G, S, row0, (j - 1) * Wd);
     });
 #pragma unroll
     for (int o = 0; o < T; ++o)
@@ -394,7 +459,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
         al.v[o][rr] = pp * d1 + gg.v[o][rr] * ad[j - 1].v[o][rr] * d2;
       }
   });
-  bstore(al, p.Alpha, S, row0, 0);
+  bstore_stream(al, p.Alpha, S, row0, 0);
 }
 
 }  // namespace dbsde

@@ -8,6 +8,11 @@ variants break the numerics on purpose -- timing only.
   nostage   each pass streams its first weight piece once, then reuses it
             without DMA or barriers (weight staging out)
   bare      nostore + noload + nostage
+  ntstore   bstore() uses nontemporal stores (streaming, no L2 allocate)
+  ntload    bload() uses nontemporal loads
+  ntsel     nontemporal stores only for arrays the weight-gradient kernel reads
+            (H, Delta, Hdot, Alpha, zbar); Abuf/G/zfull (read by phase C) cached
+  ntsel2    the complement of ntsel
 
     python tools/exp_phase.py nostore noload nostage bare
 """
@@ -34,6 +39,29 @@ def edit(src, name):
         src = src.replace("__device__ __forceinline__ void bload(Mat<TT>& m, const float* base, int ld, int row0, int col0) {",
                           "__device__ __forceinline__ void bload(Mat<TT>& m, const float* base, int ld, int row0, int col0) {\n"
                           "  if (ld > 0) { for (int t = 0; t < TT; ++t) m.v[t] = floatx4{0.f, 0.f, 0.f, 0.f}; return; }")
+    if name in ("ntstore", "ntboth"):
+        src = src.replace("  for (int t = 0; t < TT; ++t) *(floatx4*)(p + 16 * t) = m.v[t];",
+                          "  for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 16 * t));")
+    if name in ("ntload", "ntboth"):
+        src = src.replace("  for (int t = 0; t < TT; ++t) m.v[t] = *(const floatx4*)(p + 16 * t);",
+                          "  for (int t = 0; t < TT; ++t) m.v[t] = __builtin_nontemporal_load((const floatx4*)(p + 16 * t));")
+    if name in ("ntsel", "ntsel2"):
+        nt_arrays = ("p.H,", "p.Delta,", "p.Hdot,", "p.Alpha,", "p.zbar,")
+        if name == "ntsel2":
+            nt_arrays = ("p.Abuf,", "p.G,", "p.zfull,")
+        src = src.replace("__device__ __forceinline__ void bstore(const Mat<TT>& m, float* base, int ld, int row0, int col0) {",
+                          "__device__ __forceinline__ void bstore_nt(const Mat<TT>& m, float* base, int ld, int row0, int col0) {\n"
+                          "  const int lane = threadIdx.x & 63;\n"
+                          "  float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);\n"
+                          "#pragma unroll\n"
+                          "  for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 16 * t));\n}\n"
+                          "template <int TT>\n"
+                          "__device__ __forceinline__ void bstore(const Mat<TT>& m, float* base, int ld, int row0, int col0) {")
+        lines = src.split("\n")
+        for i, ln in enumerate(lines):
+            if "bstore(" in ln and "void bstore" not in ln and any(a in ln for a in nt_arrays):
+                lines[i] = ln.replace("bstore(", "bstore_nt(")
+        src = "\n".join(lines)
     if name in ("nostage", "bare"):
         src = src.replace("  __device__ __forceinline__ const floatx4* next() {\n",
                           "  __device__ __forceinline__ const floatx4* next() {\n"
