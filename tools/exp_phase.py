@@ -13,6 +13,8 @@ variants break the numerics on purpose -- timing only.
   ntsel     nontemporal stores only for arrays the weight-gradient kernel reads
             (H, Delta, Hdot, Alpha, zbar); Abuf/G/zfull (read by phase C) cached
   ntsel2    the complement of ntsel
+  quadplain quad-order stores of the weight-gradient operands without the
+            nontemporal hint
 
     python tools/exp_phase.py nostore noload nostage bare
 """
@@ -45,6 +47,12 @@ def edit(src, name):
     if name in ("ntload", "ntboth"):
         src = src.replace("  for (int t = 0; t < TT; ++t) m.v[t] = *(const floatx4*)(p + 16 * t);",
                           "  for (int t = 0; t < TT; ++t) m.v[t] = __builtin_nontemporal_load((const floatx4*)(p + 16 * t));")
+    if name == "quadplain":
+        src = src.replace("    for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 64 * t));",
+                          "    for (int t = 0; t < TT; ++t) *(floatx4*)(p + 64 * t) = m.v[t];")
+    if name == "allplain":
+        src = src.replace("__builtin_nontemporal_store(m.v[t], (floatx4*)(p + 64 * t));", "*(floatx4*)(p + 64 * t) = m.v[t];")
+        src = src.replace("__builtin_nontemporal_store(m.v[t], (floatx4*)(p + 16 * t));", "*(floatx4*)(p + 16 * t) = m.v[t];")
     if name in ("ntsel", "ntsel2"):
         nt_arrays = ("p.H,", "p.Delta,", "p.Hdot,", "p.Alpha,", "p.zbar,")
         if name == "ntsel2":
@@ -83,7 +91,9 @@ def build(name):
     open(ph, "w").write(s2)
     os.makedirs(out, exist_ok=True)
     objs = []
-    for unit, extra in (("engine.hip", []), ("evals.hip", []), ("tnw.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=true"])):
+    sys.path.insert(0, PKG)
+    from build_lib import UNITS
+    for unit, extra in UNITS:
         o = os.path.join(tmp, unit + ".o")
         subprocess.run([HIPCC, *FLAGS, *extra, "-c", "-o", o, os.path.join(csrc, unit)], check=True)
         objs.append(o)
