@@ -71,6 +71,10 @@ struct dbsde_ctx {
   hipStream_t pipe2 = nullptr;
   hipStream_t pipe_more[2] = {nullptr, nullptr};   // streams 3 and 4 (DBSDE_PIPES=3|4)
   int pipes = 2;
+  // bit i: fork_side(i) work stays on the main stream.  Default: both (the
+  // cross-stream event hops cost more than the overlap of the small prep /
+  // loss kernels gains, -12 us/step measured); DBSDE_SERIAL=0 forks them.
+  int serial = 3;
   hipEvent_t ev_pipe[2] = {nullptr, nullptr};
   hipEvent_t ev_more[2] = {nullptr, nullptr};
   hipEvent_t ev_prof[2] = {nullptr, nullptr};
@@ -109,6 +113,7 @@ struct dbsde_ctx {
   unsigned char* d_used = nullptr;
   PackDesc* d_prep = nullptr;
   int n_prep = 0;
+  int prep_blocks = 1;   // pack_tagged_kernel grid.x: one element per thread
   PackDesc* d_fin = nullptr;
   int n_fin = 0;
   std::vector<float*> slab;  // TN problem slabs (0 = x-stack, j = block j)
@@ -230,6 +235,7 @@ int run(dbsde_ctx* c, const char* name, double flops, double bytes, F&& launch) 
 // profiler's per-kernel times stay correct.
 template <class F>
 int fork_side(dbsde_ctx* c, int i, F&& f) {
+  if (c->serial >> i & 1) return f();   // in-order on the main stream (DBSDE_SERIAL bit i)
   HIPC(c, hipEventRecord(c->ev_fork[i], c->stream));
   HIPC(c, hipStreamWaitEvent(c->side, c->ev_fork[i], 0));
   hipStream_t main_stream = c->stream;
@@ -241,6 +247,7 @@ int fork_side(dbsde_ctx* c, int i, F&& f) {
   return DBSDE_OK;
 }
 int join_side(dbsde_ctx* c, int i) {
+  if (c->serial >> i & 1) return DBSDE_OK;
   HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[i], 0));
   return DBSDE_OK;
 }
@@ -333,6 +340,7 @@ int build_net(dbsde_ctx* c) {
   if (c->rho != 0.f)
     for (int j = 2; j < n - 1; ++j)
       if (L[j] != L[1]) return fail(c, DBSDE_EINVAL, "residual modes need equal hidden widths");
+  if (c->proj && L[1] > NAIS_LMAX) return fail(c, DBSDE_EINVAL, "NAIS projection supports hidden width <= 128");
   c->nparams = off;
   c->used.assign(off, 1);
   if (g.mode == DBSDE_MODE_NAIS_NET) {
@@ -511,6 +519,8 @@ int build_buffers(dbsde_ctx* c) {
   P.push_back(mk_desc(ptag(c->out.w), 1, c->wout, 1, c->out.in, 1, 0, PK_COPY));
   P.push_back(mk_desc(ptag(c->out.b), 1, c->bout, 1, 1, 1, 0, PK_COPY));
   c->n_prep = (int)P.size();
+  c->prep_blocks = 1;
+  for (const PackDesc& d : P) c->prep_blocks = std::max(c->prep_blocks, (d.rows * d.cols + 255) / 256);
 
   // ---- gradient slabs and finalize descriptors
   bool uniformW = true;
@@ -778,6 +788,7 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
   d.src2 = untag(d.src2, params, grad);
   d.dst = (float*)untag(d.dst, params, grad);
   const int total = d.rows * d.cols;
+  if ((int)blockIdx.x * 256 >= total) return;
   // NAIS projection: |RtR|_F from rtr_params_kernel's partials (fixed order)
   __shared__ float nrm_s;
   if (d.mode == PK_NEGPROJ) {
@@ -831,41 +842,29 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
     }
   }
 }
-// Small LDS-tiled SGEMM for the L x L NAIS matrices (L <= 128): one 16x16
-// output tile per 256-thread workgroup, K staged through LDS in 16-wide tiles.
-//   TRANS_A: C = A^T B (RtR = W^T W)   else: C = A B (Wbar = W S)
-template <bool TRANS_A>
-__device__ __forceinline__ float tile_gemm16(const float* A, const float* B, int L, int ti, int tj, float (*As)[17],
-                                             float (*Bs)[17]) {
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int row = ti * 16 + ty, col = tj * 16 + tx;
-  float acc = 0.f;
-  for (int k0 = 0; k0 < L; k0 += 16) {
-    const int kr = k0 + tx, kc = k0 + ty;
-    // As[ty][tx] = op(A)[row][k0+tx], Bs[ty][tx] = B[k0+ty][col]
-    if (TRANS_A)
-      As[ty][tx] = (row < L && kr < L) ? A[kr * L + row] : 0.f;
-    else
-      As[ty][tx] = (row < L && kr < L) ? A[row * L + kr] : 0.f;
-    Bs[ty][tx] = (kc < L && col < L) ? B[kc * L + col] : 0.f;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) acc += As[ty][k] * Bs[k][tx];
-    __syncthreads();
-  }
-  return acc;
-}
-
 // RtR_j = W_j^T W_j (Functions/naisnet.py:33) and per-tile partial sums of
-// squares for the Frobenius norm (fixed order).
+// squares for the Frobenius norm (fixed order).  One 16x16 output tile per
+// 256-thread workgroup; the whole 16 x L and L x 16 operand strips (L <= 128)
+// are staged in LDS with one round of independent loads (a K-tiled loop would
+// chain L/16 dependent global-load latencies).
 __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, const long long* woffs, int L,
                                                          float* const* rtr, double* part, int nblk) {
-  __shared__ float As[16][17], Bs[16][17];
+  __shared__ float As[16][NAIS_LMAX + 1];   // As[r][k] = W[k][16 ti + r]
+  __shared__ float Bs[NAIS_LMAX][17];       // Bs[k][c] = W[k][16 tj + c]
   const int j = blockIdx.y, nt = (L + 15) / 16;
   const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
   const float* W = params + woffs[j];
-  const float v = tile_gemm16<true>(W, W, L, ti, tj, As, Bs);
-  const int row = ti * 16 + (threadIdx.x >> 4), col = tj * 16 + (threadIdx.x & 15);
+  for (int e = threadIdx.x; e < 16 * L; e += 256) {
+    const int k = e >> 4, q = e & 15;
+    const int ra = 16 * ti + q, cb = 16 * tj + q;
+    As[q][k] = ra < L ? W[k * L + ra] : 0.f;
+    Bs[k][q] = cb < L ? W[k * L + cb] : 0.f;
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float v = 0.f;
+  for (int k = 0; k < L; ++k) v += As[ty][k] * Bs[k][tx];
+  const int row = ti * 16 + ty, col = tj * 16 + tx;
   double sq = 0.0;
   if (row < L && col < L) {
     rtr[j][row * L + col] = v;
@@ -892,12 +891,28 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* params,
                                                             float* const* abar, float* const* rtr, int L,
                                                             const double* norms, const double* dot_part, int dot_nblk,
                                                             float* grad) {
-  __shared__ float As[16][17], Bs[16][17];
+  __shared__ float As[16][NAIS_LMAX + 1];   // As[r][k] = W[16 ti + r][k]
+  __shared__ float Bs[NAIS_LMAX][17];       // Bs[k][c] = S[k][16 tj + c], S = Rbar + Rbar^T
   __shared__ double dot_s;
   const int j = blockIdx.y, nt = (L + 15) / 16;
   const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
   const float* Ab = abar[j];
   const float* R = rtr[j];
+  const float* W = params + woffs[j];
+  // every operand load in one round, before the scalars are known
+  constexpr int PER = NAIS_LMAX * 16 / 256;
+  float wv[PER], abs_[PER], rs[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    const int k = e >> 4, q = e & 15;
+    const int ra = 16 * ti + q, cb = 16 * tj + q;
+    const bool in = k < L;
+    wv[u] = (in && ra < L) ? W[ra * L + k] : 0.f;
+    const bool ok = in && cb < L;
+    abs_[u] = ok ? Ab[k * L + cb] + Ab[cb * L + k] : 0.f;
+    rs[u] = ok ? R[k * L + cb] + R[cb * L + k] : 0.f;
+  }
   if (threadIdx.x < 64) {   // <Abar_j, R_j> from the finalize partials, fixed-order butterfly
     double dsum = 0.0;
     for (int b = threadIdx.x; b < dot_nblk; b += 64) dsum += dot_part[(size_t)j * dot_nblk + b];
@@ -911,22 +926,20 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* params,
   const bool taken = (float)n > 0.98f;
   const float cA = taken ? (float)(0.98994949366116658 / sqrt(n)) : 1.f;
   const float cR = taken ? (float)(0.98994949366116658 / sqrt(n) * 0.5 * dot / (n * n)) : 0.f;
-  const float* W = params + woffs[j];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    const int k = e >> 4, q = e & 15;
+    if (k < L) {
+      As[q][k] = wv[u];
+      Bs[k][q] = cA * abs_[u] - cR * rs[u];
+    }
+  }
+  __syncthreads();
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int row = ti * 16 + ty, col = tj * 16 + tx;
   float acc = 0.f;
-  for (int k0 = 0; k0 < L; k0 += 16) {
-    const int kr = k0 + tx, kc = k0 + ty;
-    As[ty][tx] = (row < L && kr < L) ? W[row * L + kr] : 0.f;
-    float sv = 0.f;
-    if (kc < L && col < L)
-      sv = cA * (Ab[kc * L + col] + Ab[col * L + kc]) - cR * (R[kc * L + col] + R[col * L + kc]);
-    Bs[ty][tx] = sv;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) acc += As[ty][k] * Bs[k][tx];
-    __syncthreads();
-  }
+  for (int k = 0; k < L; ++k) acc += As[ty][k] * Bs[k][tx];
   if (row < L && col < L) grad[woffs[j] + row * L + col] = acc;
 }
 }  // namespace dbsde
@@ -942,7 +955,7 @@ int prep_weights(dbsde_ctx* c, const float* params) {
     RUN(c, "rtr", fl, 0.0,
         rtr_params_kernel<<<dim3(nblk, c->K), 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, c->proj_part, nblk));
   }
-  RUN(c, "pack_weights", 0.0, 0.0, pack_tagged_kernel<<<dim3(8, c->n_prep), 256, 0, s>>>(c->d_prep, params, nullptr));
+  RUN(c, "pack_weights", 0.0, 0.0, pack_tagged_kernel<<<dim3(c->prep_blocks, c->n_prep), 256, 0, s>>>(c->d_prep, params, nullptr));
   return DBSDE_OK;
 }
 
@@ -1258,6 +1271,7 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     if (const char* ch = getenv("DBSDE_CHUNKS")) c->chunks = std::max(1, std::min(16, atoi(ch)));
     if (const char* ch = getenv("DBSDE_CHUNK0")) c->chunk0 = atoi(ch);
     if (const char* ch = getenv("DBSDE_PIPES")) c->pipes = std::max(2, std::min(4, atoi(ch)));
+    if (const char* ch = getenv("DBSDE_SERIAL")) c->serial = atoi(ch);
     if (e != hipSuccess) rc = fail(c, DBSDE_EHIP, std::string("side stream: ") + hipGetErrorString(e));
   }
   if (rc) {

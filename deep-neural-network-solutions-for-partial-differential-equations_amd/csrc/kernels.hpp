@@ -597,6 +597,7 @@ __global__ void __launch_bounds__(256) fill_col0_kernel(float* buf, int ld, long
 // Descriptor-driven gather/scatter (weight packing, gradient finalize)
 // --------------------------------------------------------------------------
 enum PackMode { PK_COPY = 0, PK_ADD2 = 1, PK_NEGPROJ = 2, PK_SLABSUM = 3 };
+constexpr int NAIS_LMAX = 128;   // NAIS projection matrices: L x L, L <= 128 (rtr / proj kernels)
 struct PackDesc {
   const float* src;
   const float* src2;   // PK_ADD2 second source
@@ -793,14 +794,19 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
     cc = e - r * d.cols;
     const float* src = d.src + (size_t)r * d.src_ld + cc;
     const int k0 = grp * d.nslab / 4, k1 = (grp + 1) * d.nslab / 4;
-    double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    // 32 slabs per round, all loads in flight before the (fixed-order) sum
     int k = k0;
-    for (; k + 8 <= k1; k += 8) {
+    for (; k + 32 <= k1; k += 32) {
+      float x[32];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) sa[u] += src[(size_t)(k + u) * d.slab_stride];
+      for (int u = 0; u < 32; ++u) x[u] = src[(size_t)(k + u) * d.slab_stride];
+      double q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        q[u] = ((double)x[4 * u] + (double)x[4 * u + 1]) + ((double)x[4 * u + 2] + (double)x[4 * u + 3]);
+      s += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     }
-    for (; k < k1; ++k) sa[0] += src[(size_t)k * d.slab_stride];
-    s = ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7]));
+    for (; k < k1; ++k) s += src[(size_t)k * d.slab_stride];
   }
   __shared__ double part[4][64];
   part[grp][lane] = s;
