@@ -142,10 +142,22 @@ struct PieceStager {
   const float* const* img;
   const int* nf;
   int n, st, wave, lane, buf;
+#ifdef DBSDE_STAMPS   // diagnostic build (tools/exp_phase.py stamps): per-piece s_memtime
+  unsigned long long ts[3 * 32];
+  __device__ __forceinline__ void mark() { ts[3 * (st - 1) + 2] = __builtin_amdgcn_s_memtime(); }
+#else
+  __device__ __forceinline__ void mark() {}
+#endif
   template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
+#ifdef DBSDE_STAMPS
+    ts[3 * st] = __builtin_amdgcn_s_memtime();
+#endif
     vm_wait<NYOUNG>();
     lds_barrier();
+#ifdef DBSDE_STAMPS
+    ts[3 * st + 1] = __builtin_amdgcn_s_memtime();
+#endif
     if (st + 1 < n) piece_dma(img[st + 1], nf[st + 1], wl + ((st + 1) & 1) * buf, wave, lane);
     // nothing issued later may be hoisted above the DMA (the NYOUNG counts)
     __builtin_amdgcn_sched_barrier(0);
@@ -154,6 +166,21 @@ struct PieceStager {
     return cur;
   }
 };
+
+#ifdef DBSDE_STAMPS
+__device__ __forceinline__ void stamp_dump(const PieceStager& sg, char kind, int tile) {
+  const unsigned long long tend = __builtin_amdgcn_s_memtime();
+  if ((tile == 5 || tile == 405 || tile == 805) && (threadIdx.x & 63) == 0)
+    for (int i = 0; i < sg.n; ++i) {
+      const unsigned long long nx = i + 1 < sg.n ? sg.ts[3 * i + 3] : tend;
+      printf("STAMP %c %d %d %d wait %llu mfma %llu post %llu\n", kind, tile, sg.wave, i, sg.ts[3 * i + 1] - sg.ts[3 * i],
+             sg.ts[3 * i + 2] - sg.ts[3 * i + 1], nx - sg.ts[3 * i + 2]);
+    }
+}
+#define STAMP_DUMP(kind) stamp_dump(sg, kind, tile)
+#else
+#define STAMP_DUMP(kind)
+#endif
 
 struct NoOp {
   __device__ __forceinline__ void operator()() const {}
@@ -172,9 +199,11 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceSt
   // sinks them to the end of the piece, right in front of the next vmcnt(0)
   __builtin_amdgcn_sched_barrier(0);
   sgemm_piece<TO, TI, 0, H>(acc, b, w, lane);
+  sg.mark();
   if constexpr (H < TI) {
     w = sg.template next<NAFTER>();
     sgemm_piece<TO, TI, H, TI>(acc, b, w, lane);
+    sg.mark();
   }
 }
 
@@ -336,6 +365,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
     *(floatx4*)o = floatx4{v6[0], v6[1], v6[2], v6[3]};
     *(floatx4*)(o + 4) = floatx4{v6[4], v6[5], umask, 0.f};
   }
+  STAMP_DUMP('A');
 }
 
 // ---------------------------------------------------------------------------
@@ -460,6 +490,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
       }
   });
   bstore_stream(al, p.Alpha, S, row0, 0);
+  STAMP_DUMP('C');
 }
 
 }  // namespace dbsde

@@ -13,6 +13,8 @@ variants break the numerics on purpose -- timing only.
   ntsel     nontemporal stores only for arrays the weight-gradient kernel reads
             (H, Delta, Hdot, Alpha, zbar); Abuf/G/zfull (read by phase C) cached
   ntsel2    the complement of ntsel
+  stamps    -DDBSDE_STAMPS: per-piece s_memtime (wait / MFMA issue / post)
+            printed for three tiles -- diagnostic only
   quadplain quad-order stores of the weight-gradient operands without the
             nontemporal hint
 
@@ -86,16 +88,20 @@ def build(name):
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
     ph = os.path.join(csrc, "phase.hpp")
     s = open(ph).read()
-    s2 = edit(s, name)
-    assert s2 != s, name
-    open(ph, "w").write(s2)
+    defs = []
+    if name == "stamps":    # per-piece s_memtime printf of three tiles (diagnostic build)
+        defs = ["-DDBSDE_STAMPS"]
+    else:
+        s2 = edit(s, name)
+        assert s2 != s, name
+        open(ph, "w").write(s2)
     os.makedirs(out, exist_ok=True)
     objs = []
     sys.path.insert(0, PKG)
     from build_lib import UNITS
     for unit, extra in UNITS:
         o = os.path.join(tmp, unit + ".o")
-        subprocess.run([HIPCC, *FLAGS, *extra, "-c", "-o", o, os.path.join(csrc, unit)], check=True)
+        subprocess.run([HIPCC, *FLAGS, *extra, *defs, "-c", "-o", o, os.path.join(csrc, unit)], check=True)
         objs.append(o)
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", os.path.join(out, "libdbsde.so"), *objs],
                    check=True)
