@@ -107,23 +107,58 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // acc[o] += sum_{t in [T0, T1)} W(o, t) . b(t); img = the piece holding
-// fragment (o, t) at ((t - T0) * TO + o).  Output blocks in groups of OG
-// (OG >= 2 keeps consecutive MFMAs on independent accumulators).
-template <int TO, int TI, int T0, int T1, int OG = 4>
+// fragment (o, t) at ((t - T0) * TO + o).
+//   PF: the piece's fragments in that order, two per group (consecutive
+//   fragments have different output blocks, so consecutive MFMAs never share
+//   an accumulator), the next group's two ds_read_b128 issued before this
+//   group's 8 MFMAs -- the LDS latency hides under 256 matrix-pipe cycles.
+//   Otherwise output blocks in groups of 4 per input block, reads just ahead
+//   of use (fewer live registers: phase C is at the 256-VGPR limit).
+template <int TO, int TI, int T0, int T1, bool PF>
 __device__ __forceinline__ void sgemm_piece(Mat<TO>& acc, const Mat<TI>& b, const floatx4* img, int lane) {
+  if constexpr (PF) {
+    constexpr int NF = (T1 - T0) * TO, NG = (NF + 1) / 2;
+    floatx4 w[2][2];
 #pragma unroll
-  for (int t = T0; t < T1; ++t) {
+    for (int k = 0; k < 2; ++k)
+      if (k < NF) w[0][k] = img[k * 64 + lane];
 #pragma unroll
-    for (int o0 = 0; o0 < TO; o0 += OG) {
-      floatx4 w[OG];
+    for (int g = 0; g < NG; ++g) {
+      if (g + 1 < NG) {
 #pragma unroll
-      for (int o = 0; o < OG; ++o)
-        if (o0 + o < TO) w[o] = img[((t - T0) * TO + o0 + o) * 64 + lane];
+        for (int k = 0; k < 2; ++k) {
+          const int f = 2 * (g + 1) + k;
+          if (f < NF) w[(g + 1) & 1][k] = img[f * 64 + lane];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this group's MFMAs
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int f = 2 * g + k;
+          if (f < NF) {
+            const int t = T0 + f / TO, o = f % TO;
+            acc.v[o] = mfma4(w[g & 1][k][r], b.v[t][r], acc.v[o]);
+          }
+        }
+    }
+  } else {
+    constexpr int OG = 4;
+#pragma unroll
+    for (int t = T0; t < T1; ++t) {
+#pragma unroll
+      for (int o0 = 0; o0 < TO; o0 += OG) {
+        floatx4 w[OG];
+#pragma unroll
         for (int o = 0; o < OG; ++o)
-          if (o0 + o < TO) acc.v[o0 + o] = mfma4(w[o][r], b.v[t][r], acc.v[o0 + o]);
+          if (o0 + o < TO) w[o] = img[((t - T0) * TO + o0 + o) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int o = 0; o < OG; ++o)
+            if (o0 + o < TO) acc.v[o0 + o] = mfma4(w[o][r], b.v[t][r], acc.v[o0 + o]);
+      }
     }
   }
 }
@@ -190,7 +225,7 @@ struct NoOp {
 // right after the first piece's barrier (deferred stores, early loads).
 // NPRE = vector-memory ops issued since the first piece's DMA (the previous
 // stage's epilogue), NAFTER = the ops `after` issues (both lower bounds).
-template <int TO, int TI, int NPRE, int NAFTER, class F>
+template <int TO, int TI, int NPRE, int NAFTER, bool PF = false, class F>
 __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceStager& sg, int lane, F&& after) {
   constexpr int H = (TI + 1) / 2;
   const floatx4* w = sg.template next<NPRE>();
@@ -198,11 +233,11 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceSt
   // keep the deferred stores / early loads here: left to itself the scheduler
   // sinks them to the end of the piece, right in front of the next vmcnt(0)
   __builtin_amdgcn_sched_barrier(0);
-  sgemm_piece<TO, TI, 0, H>(acc, b, w, lane);
+  sgemm_piece<TO, TI, 0, H, PF>(acc, b, w, lane);
   sg.mark();
   if constexpr (H < TI) {
     w = sg.template next<NAFTER>();
-    sgemm_piece<TO, TI, H, TI>(acc, b, w, lane);
+    sgemm_piece<TO, TI, H, TI, PF>(acc, b, w, lane);
     sg.mark();
   }
 }
@@ -213,6 +248,7 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceSt
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT>
 __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
+  constexpr bool PFA = true;    // group-ahead fragment prefetch (sgemm_piece)
   constexpr int TB = T > TD ? T : TD, BUF = ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[2 * BUF];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
@@ -228,7 +264,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   Mat<T> s1[K + 1];   // act'(a_j)
   Mat<T> h, acc;
   zero(acc);
-  stage_mm<T, TD, TD, 0>(acc, x, sg, lane, NoOp{});
+  stage_mm<T, TD, TD, 0, PFA>(acc, x, sg, lane, NoOp{});
   fstore(acc, p.Abuf, S, row0, 0);
 #pragma unroll
   for (int o = 0; o < T; ++o)
@@ -242,8 +278,8 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero(acc);
-    stage_mm<T, T, T, T>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd); });
-    if (p.has_v) stage_mm<T, TD, 0, 0>(acc, x, sg, lane, NoOp{});
+    stage_mm<T, T, T, T, PFA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd); });
+    if (p.has_v) stage_mm<T, TD, 0, 0, PFA>(acc, x, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o) {
       const floatx4 bb = p.has_v ? floatx4{0.f, 0.f, 0.f, 0.f} : *(const floatx4*)(p.beta[j - 1] + 16 * o + 4 * q);
@@ -305,10 +341,10 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
     zero(gn);
     constexpr int NPREV = j < K ? 2 * T : T;
     if (p.has_v) {
-      stage_mm<TD, T, 0, NPREV>(z, dl, sg, lane, prev);   // Z += delta_j V_j
-      stage_mm<T, T, 0, 0>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
+      stage_mm<TD, T, 0, NPREV, PFA>(z, dl, sg, lane, prev);   // Z += delta_j V_j
+      stage_mm<T, T, 0, 0, PFA>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
     } else {
-      stage_mm<T, T, 0, NPREV>(gn, dl, sg, lane, prev);
+      stage_mm<T, T, 0, NPREV, PFA>(gn, dl, sg, lane, prev);
     }
 #pragma unroll
     for (int o = 0; o < T; ++o)
@@ -319,7 +355,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
         dl.v[o][r] = gv * s1[j - 1].v[o][r];
       }
   });
-  stage_mm<TD, T, 0, 2 * T + TD>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
+  stage_mm<TD, T, 0, 2 * T + TD, PFA>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
     fstore(g, p.G, S, row0, 0);
     bstore_stream(dl, p.Delta, S, row0, 0);
     bload(x, p.xin, p.Dp, row0, 0);
@@ -374,6 +410,13 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT>
 __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
+#ifndef DBSDE_PFC_T
+#define DBSDE_PFC_T true
+#endif
+#ifndef DBSDE_PFC_R
+#define DBSDE_PFC_R false
+#endif
+  constexpr bool PFC_T = DBSDE_PFC_T, PFC_R = DBSDE_PFC_R;   // prefetch in the tangent / reverse stages
   constexpr int TB = T > TD ? T : TD, BUF = ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[2 * BUF];
   __shared__ double lsum[P3_WAVES];
@@ -431,7 +474,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   Mat<T> ad[K + 1];   // adot_j
   Mat<T> hd, av;
   zero(ad[0]);
-  stage_mm<T, TD, TD, T>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
+  stage_mm<T, TD, TD, T, PFC_T>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
     fload(av, p.Abuf, S, row0, 0);
     if (threadIdx.x == 0) p.loss_part[tile] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
   });
@@ -442,11 +485,11 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero(ad[j]);
-    stage_mm<T, T, 0, 2 * T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
+    stage_mm<T, T, 0, 2 * T, PFC_T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
       bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd);
       fload(av, p.Abuf, S, row0, j * Wd);
     });
-    if (p.has_v) stage_mm<T, TD, 0, 0>(ad[j], zb, sg, lane, NoOp{});
+    if (p.has_v) stage_mm<T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
@@ -473,7 +516,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
     constexpr int j = K - decltype(ic)::value;
     Mat<T> acc, gg;
     zero(acc);
-    stage_mm<T, T, 0, 3 * T>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
+    stage_mm<T, T, 0, 3 * T, PFC_R>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
       bstore_stream(al, p.Alpha, S, row0, j * Wd);
       fload(av, p.Abuf, S, row0, (j - 1) * Wd);
       fload(gg, p.G, S, row0, (j - 1) * Wd);

@@ -13,6 +13,8 @@ variants break the numerics on purpose -- timing only.
   ntsel     nontemporal stores only for arrays the weight-gradient kernel reads
             (H, Delta, Hdot, Alpha, zbar); Abuf/G/zfull (read by phase C) cached
   ntsel2    the complement of ntsel
+  noslp     -fno-slp-vectorize (no v_pk_* f32 packing)
+  pfcr      group-ahead fragment prefetch in phase C's reverse stages too
   stamps    -DDBSDE_STAMPS: per-piece s_memtime (wait / MFMA issue / post)
             printed for three tiles -- diagnostic only
   quadplain quad-order stores of the weight-gradient operands without the
@@ -91,6 +93,10 @@ def build(name):
     defs = []
     if name == "stamps":    # per-piece s_memtime printf of three tiles (diagnostic build)
         defs = ["-DDBSDE_STAMPS"]
+    elif name == "noslp":   # no SLP packing of f32 elementwise work into v_pk_* (MI355X_MICROARCH: anti-lever beside MFMA)
+        defs = ["-fno-slp-vectorize"]
+    elif name == "pfcr":    # prefetch also in phase C's reverse stages (spills 4 VGPRs)
+        defs = ["-DDBSDE_PFC_R=true"]
     else:
         s2 = edit(s, name)
         assert s2 != s, name
