@@ -256,19 +256,24 @@ int join_side(dbsde_ctx* c, int i) {
 // ---------------------------------------------------------------------------
 // fused phase-kernel instantiations: (level tiles T, D tiles TD, blocks K)
 struct FusedVariant {
-  int T, TD, K, act;
+  int T, TD, K, act, hv;
   void (*A)(FusedArgs);
   void (*C)(FusedArgs);
 };
-#define FV(T, TD, K, ACT) {T, TD, K, ACT, phaseA_kernel<T, TD, K, ACT>, phaseC_kernel<T, TD, K, ACT>}
+// HV: the network has the NAIS x-stack (V_j); a template flag, so each kernel
+// carries only its own code path (smaller straight-line kernels)
+#define FV(T, TD, K, ACT, HV) {T, TD, K, ACT, HV, phaseA_kernel<T, TD, K, ACT, HV>, phaseC_kernel<T, TD, K, ACT, HV>}
+#define FV2(T, TD, K, ACT) FV(T, TD, K, ACT, true), FV(T, TD, K, ACT, false)
 const FusedVariant kFused[] = {
-    FV(7, 7, 3, 0), FV(7, 7, 3, 1), FV(7, 7, 3, 2), FV(1, 1, 1, 0), FV(1, 1, 1, 1), FV(1, 1, 1, 2),
-    FV(1, 1, 2, 0), FV(1, 1, 2, 1), FV(1, 1, 2, 2), FV(1, 1, 3, 0), FV(1, 1, 3, 1), FV(1, 1, 3, 2),
+    FV2(7, 7, 3, 0), FV2(7, 7, 3, 1), FV2(7, 7, 3, 2), FV2(1, 1, 1, 0), FV2(1, 1, 1, 1), FV2(1, 1, 1, 2),
+    FV2(1, 1, 2, 0), FV2(1, 1, 2, 1), FV2(1, 1, 2, 2), FV2(1, 1, 3, 0), FV2(1, 1, 3, 1), FV2(1, 1, 3, 2),
 };
+#undef FV2
 #undef FV
-int fused_variant(int T, int TD, int K, int act) {
+int fused_variant(int T, int TD, int K, int act, bool hv) {
   for (int i = 0; i < (int)(sizeof(kFused) / sizeof(kFused[0])); ++i)
-    if (kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act) return i;
+    if (kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv)
+      return i;
   return -1;
 }
 
@@ -367,7 +372,7 @@ int build_net(dbsde_ctx* c) {
   for (int j = 1; j <= c->K; ++j) uniform = uniform && c->Wp[j] == c->Wp[0];
   const char* env = getenv("DBSDE_FUSED");
   const bool allow = !(env && env[0] == '0');
-  c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act) >= 0;
+  c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v) >= 0;
   // problem kind: Brownian dimension, g columns, u clamp
   const dbsde_problem& pr = g.problem;
   if (pr.kind != DBSDE_PROB_DIAG && pr.kind != DBSDE_PROB_HESTON) return fail(c, DBSDE_EINVAL, "unknown problem kind");
@@ -1356,7 +1361,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
 
   int nloss_parts;
   FusedArgs fa;
-  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act) : -1;
+  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act, c->has_v) : -1;
   if (fv >= 0) {
     fa = fused_args(c, R, Rp, N1, q3);
     const int nv = nv_x(c);

@@ -136,6 +136,7 @@ struct RowCotan {
   bool valid, term;
   int n;
   float res, ub, coefY, dt, gsc, mask, q3s;
+  float gA, gB;   // terminal: d g / d x_col = gA x_col + gB (terminal_dg as an affine map)
 };
 __device__ __forceinline__ RowCotan row_cotan(const CotanParams& p, int r) {
   RowCotan c{};
@@ -155,6 +156,8 @@ __device__ __forceinline__ RowCotan row_cotan(const CotanParams& p, int r) {
   if (term) {
     c.res = y - terminal_g(p.g_kind, a0[3], a1[0], p.gcols, p.strike, p.g_alpha, c.gsc);
     c.ub = 2.f * c.res;
+    c.gA = p.g_kind == 0 ? 2.f : (p.g_kind == 3 ? c.gsc : 0.f);
+    c.gB = (p.g_kind == 0 || p.g_kind == 3) ? 0.f : c.gsc;
   } else {
     c.dt = tn - t;
     c.res = step_residual(p, a0, a1, y, yn, c.dt, q);
@@ -169,17 +172,18 @@ __device__ __forceinline__ RowCotan row_cotan(const CotanParams& p, int r) {
 }
 // zbar of column col (1 <= col <= D) from x, z, (sigma dW) of that column;
 // tz accumulates the terminal |Z - grad g|^2 over the g columns
+// Branch-free (both row kinds evaluated, then selected): straight-line code
+// per element, no divergence between terminal and interior rows of a wave.
 __device__ __forceinline__ float col_zbar(const CotanParams& p, const RowCotan& c, int col, float xv, float zv,
                                           float sv, float& tz) {
-  if (!c.term) {
-    const float dphidz = -p.phi_r * p.phi_c * xv + 2.f * p.phi_zz * zv;
-    const float sd = p.q3S ? c.q3s : sv;
-    return c.mask * (c.coefY * (dphidz * c.dt + sd));
-  }
-  if (col > p.gcols) return 0.f;
-  const float e = zv - terminal_dg(p.g_kind, xv, c.gsc);
-  tz += e * e;
-  return c.mask * (2.f * e);
+  const float dphidz = -p.phi_r * p.phi_c * xv + 2.f * p.phi_zz * zv;
+  const float sd = p.q3S ? c.q3s : sv;
+  const float vn = c.mask * (c.coefY * (dphidz * c.dt + sd));
+  const float e = zv - (c.gA * xv + c.gB);
+  const bool ing = col <= p.gcols;
+  tz += (c.term && ing) ? e * e : 0.f;
+  const float vt = ing ? c.mask * (2.f * e) : 0.f;
+  return c.term ? vt : vn;
 }
 
 // Forward-only loss (predict / loss_function without backward): per-block

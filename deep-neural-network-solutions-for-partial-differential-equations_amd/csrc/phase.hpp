@@ -246,7 +246,7 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceSt
 // phase A: forward + input gradient + Z (+ residual row sums)
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, {[Z_j], B_j} j=K..1, Z0
 // ---------------------------------------------------------------------------
-template <int T, int TD, int K, int ACT>
+template <int T, int TD, int K, int ACT, bool HV>
 __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   constexpr bool PFA = true;    // group-ahead fragment prefetch (sgemm_piece)
   constexpr int TB = T > TD ? T : TD, BUF = ((TB + 1) / 2) * TB * 64;
@@ -279,12 +279,14 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
     constexpr int j = decltype(jc)::value;
     zero(acc);
     stage_mm<T, T, T, T, PFA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd); });
-    if (p.has_v) stage_mm<T, TD, 0, 0, PFA>(acc, x, sg, lane, NoOp{});
+    if constexpr (HV) stage_mm<T, TD, 0, 0, PFA>(acc, x, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o) {
-      const floatx4 bb = p.has_v ? floatx4{0.f, 0.f, 0.f, 0.f} : *(const floatx4*)(p.beta[j - 1] + 16 * o + 4 * q);
+      if constexpr (!HV) {
+        const floatx4 bb = *(const floatx4*)(p.beta[j - 1] + 16 * o + 4 * q);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc.v[o][r] += bb[r];
+        for (int r = 0; r < 4; ++r) acc.v[o][r] += bb[r];
+      }
     }
     fstore(acc, p.Abuf, S, row0, j * Wd);
 #pragma unroll
@@ -340,7 +342,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
     Mat<T> gn;
     zero(gn);
     constexpr int NPREV = j < K ? 2 * T : T;
-    if (p.has_v) {
+    if constexpr (HV) {
       stage_mm<TD, T, 0, NPREV, PFA>(z, dl, sg, lane, prev);   // Z += delta_j V_j
       stage_mm<T, T, 0, 0, PFA>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
     } else {
@@ -408,7 +410,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
 // phase C: cotangents + forward tangent along zbar + reverse over (primal, tangent)
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, B_j j=K..1
 // ---------------------------------------------------------------------------
-template <int T, int TD, int K, int ACT>
+template <int T, int TD, int K, int ACT, bool HV>
 __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
 #ifndef DBSDE_PFC_T
 #define DBSDE_PFC_T true
@@ -489,7 +491,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
       bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd);
       fload(av, p.Abuf, S, row0, j * Wd);
     });
-    if (p.has_v) stage_mm<T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
+    if constexpr (HV) stage_mm<T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
