@@ -75,7 +75,8 @@ struct dbsde_ctx {
   // cross-stream event hops cost more than the overlap of the small prep /
   // loss kernels gains, -12 us/step measured); DBSDE_SERIAL=0 forks them.
   int serial = 3;
-  int phase_pad = 0;   // extra dynamic LDS per phase workgroup (occupancy experiments, DBSDE_PHASE_PAD bytes)
+  int phase_pad = 0;
+  bool rollout_fast = true;   // rollout_fast_kernel for diagonal device-Philox rollouts (DBSDE_ROLLOUT_FAST=0: off)   // extra dynamic LDS per phase workgroup (occupancy experiments, DBSDE_PHASE_PAD bytes)
   hipEvent_t ev_pipe[2] = {nullptr, nullptr};
   hipEvent_t ev_more[2] = {nullptr, nullptr};
   hipEvent_t ev_prof[2] = {nullptr, nullptr};
@@ -110,7 +111,8 @@ struct dbsde_ctx {
   float** d_abar = nullptr;
   double* proj_part = nullptr;
   double* dot_part = nullptr;     // <Abar_j, R_j> partials from the gradient finalize (one per 64 elements)
-  int dot_nblk = 0;
+  int dot_nblk = 0;               // partials slots per block (stride)
+  int dot_nused = 0;              // partials the finalize writes (tilefin: one per 256 tile elements)
   unsigned char* d_used = nullptr;
   PackDesc* d_prep = nullptr;
   int n_prep = 0;
@@ -443,6 +445,7 @@ int build_buffers(dbsde_ctx* c) {
     if ((rc = dalloc_t(c, &c->proj_part, (size_t)K * std::max((LW * LW + 255) / 256, ((LW + 15) / 16) * ((LW + 15) / 16)))))
       return rc;
     c->dot_nblk = (LW * LW + 63) / 64;
+    c->dot_nused = c->dot_nblk;   // tnw layouts override below
     if ((rc = dalloc_t(c, &c->dot_part, (size_t)K * c->dot_nblk))) return rc;
     if ((rc = dalloc_t(c, &c->d_rtr, K))) return rc;
     if ((rc = dalloc_t(c, &c->d_abar, K))) return rc;
@@ -540,12 +543,19 @@ int build_buffers(dbsde_ctx* c) {
     const int T = Dp, P = 2 * K + 2, S = c->tnw_S;
     c->tnw_nb = T / 16;
     c->tnw_P = P;
+    if (c->proj) {
+      c->dot_nused = (T * T + TF_ELEMS - 1) / TF_ELEMS;
+      if (c->dot_nused > c->dot_nblk) return fail(c, DBSDE_EINVAL, "internal: dot partials");
+    }
     if ((rc = dalloc_t(c, &c->slabW, (size_t)S * P * T * T))) return rc;
     auto wsum = [&](int p, int r0, int c0, int rows, int cols, float* dst, int dst_ld, float scale) {
       PackDesc d = mk_desc(c->slabW + (size_t)p * T * T + (size_t)r0 * T + c0, T, dst, dst_ld, rows, cols, 0,
                            PK_SLABSUM, scale);
       d.nslab = S;
       d.slab_stride = (long long)P * T * T;
+      d.sp = p;
+      d.sr0 = r0;
+      d.sc0 = c0;
       F.push_back(d);
     };
     // x-stack problems p = j (input layer, V_j), block problems p = K + j (B_j)
@@ -896,6 +906,7 @@ __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, co
 __global__ void __launch_bounds__(256) proj_backward_kernel(const float* params, const long long* woffs,
                                                             float* const* abar, float* const* rtr, int L,
                                                             const double* norms, const double* dot_part, int dot_nblk,
+                                                            int dot_nused,
                                                             float* grad) {
   __shared__ float As[16][NAIS_LMAX + 1];   // As[r][k] = W[16 ti + r][k]
   __shared__ float Bs[NAIS_LMAX][17];       // Bs[k][c] = S[k][16 tj + c], S = Rbar + Rbar^T
@@ -921,7 +932,7 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* params,
   }
   if (threadIdx.x < 64) {   // <Abar_j, R_j> from the finalize partials, fixed-order butterfly
     double dsum = 0.0;
-    for (int b = threadIdx.x; b < dot_nblk; b += 64) dsum += dot_part[(size_t)j * dot_nblk + b];
+    for (int b = threadIdx.x; b < dot_nused; b += 64) dsum += dot_part[(size_t)j * dot_nblk + b];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o);
     if (threadIdx.x == 0) dot_s = dsum;
@@ -1017,13 +1028,20 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp) {
 
 int finalize_grads(dbsde_ctx* c, const float* params, float* grad) {
   hipStream_t s = c->stream;
-  RUN(c, "grad_finalize", 0.0, 0.0, slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad));
+  if (c->tnw) {
+    const int T = c->Dp;
+    RUN(c, "grad_finalize", 0.0, 0.0,
+        tilefin_kernel<<<dim3((T * T + TF_ELEMS - 1) / TF_ELEMS, c->tnw_P + 1), 256, 0, s>>>(
+            c->d_fin, c->n_fin, c->slabW, c->tnw_S, c->tnw_P, T, grad));
+  } else {
+    RUN(c, "grad_finalize", 0.0, 0.0, slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad));
+  }
   if (c->proj) {
     const int LW = c->L[1];
     const int ntile = ((LW + 15) / 16) * ((LW + 15) / 16);
     RUN(c, "proj_backward", 2.0 * c->K * LW * (double)LW * LW, 0.0,
         proj_backward_kernel<<<dim3(ntile, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_abar, c->d_rtr, LW, c->norms,
-                                                               c->dot_part, c->dot_nblk, grad));
+                                                               c->dot_part, c->dot_nblk, c->dot_nused, grad));
   }
   return DBSDE_OK;
 }

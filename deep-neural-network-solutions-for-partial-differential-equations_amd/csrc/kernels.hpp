@@ -621,6 +621,7 @@ struct PackDesc {
   float* fdst;
   int ftin, frow0, fcol0;
   int ftout;           // > 0: t-major image (phase3.hpp), fragment (o, t) at t * ftout + o
+  int sp, sr0, sc0;    // tilefin_kernel: the window's problem tile and its first row / column
 };
 // float offset of W[o][i] in a fragment image with tin input / tout output
 // blocks: fragment (o/16, i/16) -- o-major (phase.hpp) or, when tout > 0,
@@ -828,6 +829,93 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
       for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
       if (lane == 0) d.dot_part[blockIdx.x] = dp;
     }
+  }
+}
+
+// Weight-gradient finalize of the wave-owned tiles (tnw.hpp): one pass over
+// each problem's T x T slab tile, float4 per lane (whole 128-byte lines, no
+// descriptor-window overfetch), the S slabs split over the 4 waves and summed
+// in fp64 in a fixed order; each summed element is then scattered to every
+// descriptor window that covers it (W, biases, Abar + its <Abar, R> partial).
+// grid (ceil(T*T / 256), P + 1): y = P zero-fills the nslab == 0 windows.
+constexpr int TF_ELEMS = 256;   // elements per block (64 lanes x float4)
+__global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int ndesc, const float* slab, int S,
+                                                      int P, int T, float* grad) {
+  const int p = blockIdx.y;
+  if (p == P) {   // zero windows (NAIS-Net's never-used input_layers[K])
+    for (int i = 0; i < ndesc; ++i) {
+      const PackDesc& d = descs[i];
+      if (d.nslab != 0) continue;
+      uintptr_t dv = (uintptr_t)d.dst;
+      float* dst = (dv & ((uintptr_t)1 << 61)) ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
+      const int total = d.rows * d.cols;
+      for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) dst[e] = 0.f;
+    }
+    return;
+  }
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int TT = T * T;
+  const int e0 = blockIdx.x * TF_ELEMS + 4 * lane;   // T % 4 == 0: the float4 stays in one row
+  const long long stride = (long long)P * TT;
+  double s4[4] = {0.0, 0.0, 0.0, 0.0};
+  if (e0 < TT) {
+    const float* src = slab + (size_t)p * TT + e0;
+    const int k0 = grp * S / 4, k1 = (grp + 1) * S / 4;
+    int k = k0;
+    for (; k + 16 <= k1; k += 16) {
+      floatx4 x[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) x[u] = *(const floatx4*)(src + (size_t)(k + u) * stride);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        double q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          q[u] = ((double)x[4 * u][c] + (double)x[4 * u + 1][c]) + ((double)x[4 * u + 2][c] + (double)x[4 * u + 3][c]);
+        s4[c] += (q[0] + q[1]) + (q[2] + q[3]);
+      }
+    }
+    for (; k < k1; ++k) {
+      const floatx4 x = *(const floatx4*)(src + (size_t)k * stride);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s4[c] += (double)x[c];
+    }
+  }
+  __shared__ double part[4][4][64];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) part[grp][c][lane] = s4[c];
+  __syncthreads();
+  if (grp != 0) return;
+  double dp = 0.0;
+  const PackDesc* dotd = nullptr;
+  if (e0 < TT) {
+    const int r = e0 / T, c00 = e0 - r * T;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const double v = (part[0][c][lane] + part[1][c][lane]) + (part[2][c][lane] + part[3][c][lane]);
+      const int cc = c00 + c;
+      for (int i = 0; i < ndesc; ++i) {
+        const PackDesc& d = descs[i];
+        if (d.nslab == 0 || d.sp != p) continue;
+        const int rr = r - d.sr0, ck = cc - d.sc0;
+        if (rr < 0 || rr >= d.rows || ck < 0 || ck >= d.cols) continue;
+        const float fv = d.scale * (float)v;
+        uintptr_t dv = (uintptr_t)d.dst;
+        float* dst = (dv & ((uintptr_t)1 << 61)) ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
+        if (d.transpose)
+          dst[(size_t)ck * d.dst_ld + rr] = fv;
+        else
+          dst[(size_t)rr * d.dst_ld + ck] = fv;
+        if (d.dotR) dp += (double)fv * (double)d.dotR[(size_t)rr * d.dst_ld + ck];
+      }
+    }
+  }
+  for (int i = 0; i < ndesc; ++i)
+    if (descs[i].nslab != 0 && descs[i].sp == p && descs[i].dotR) dotd = &descs[i];
+  if (dotd) {   // fixed-order wave reduction of the block's <Abar, R> partial
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
+    if (lane == 0) dotd->dot_part[blockIdx.x] = dp;
   }
 }
 
