@@ -75,8 +75,7 @@ struct dbsde_ctx {
   // cross-stream event hops cost more than the overlap of the small prep /
   // loss kernels gains, -12 us/step measured); DBSDE_SERIAL=0 forks them.
   int serial = 3;
-  int phase_pad = 0;
-  bool rollout_fast = true;   // rollout_fast_kernel for diagonal device-Philox rollouts (DBSDE_ROLLOUT_FAST=0: off)   // extra dynamic LDS per phase workgroup (occupancy experiments, DBSDE_PHASE_PAD bytes)
+  int phase_pad = 0;   // extra dynamic LDS per phase workgroup (occupancy experiments, DBSDE_PHASE_PAD bytes)
   hipEvent_t ev_pipe[2] = {nullptr, nullptr};
   hipEvent_t ev_more[2] = {nullptr, nullptr};
   hipEvent_t ev_prof[2] = {nullptr, nullptr};
