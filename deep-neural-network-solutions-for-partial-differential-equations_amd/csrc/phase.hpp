@@ -185,6 +185,11 @@ struct PieceStager {
 #endif
   template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
+#if defined(DBSDE_PRIO_EPI)
+    __builtin_amdgcn_s_setprio(0);   // experiment: epilogues at priority 1, MFMA segments at 0
+#elif defined(DBSDE_PRIO_MFMA)
+    __builtin_amdgcn_s_setprio(1);
+#endif
 #ifdef DBSDE_STAMPS
     ts[3 * st] = __builtin_amdgcn_s_memtime();
 #endif
@@ -240,6 +245,11 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceSt
     sgemm_piece<TO, TI, H, TI, PF>(acc, b, w, lane);
     sg.mark();
   }
+#if defined(DBSDE_PRIO_EPI)
+  __builtin_amdgcn_s_setprio(1);
+#elif defined(DBSDE_PRIO_MFMA)
+  __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -95,6 +95,10 @@ def build(name):
         defs = ["-DDBSDE_STAMPS"]
     elif name == "noslp":   # no SLP packing of f32 elementwise work into v_pk_* (MI355X_MICROARCH: anti-lever beside MFMA)
         defs = ["-fno-slp-vectorize"]
+    elif name == "prioepi":   # s_setprio 1 in epilogues, 0 in MFMA segments
+        defs = ["-DDBSDE_PRIO_EPI"]
+    elif name == "priomfma":  # the opposite
+        defs = ["-DDBSDE_PRIO_MFMA"]
     elif name == "pfcr":    # prefetch also in phase C's reverse stages (spills 4 VGPRs)
         defs = ["-DDBSDE_PFC_R=true"]
     else:
