@@ -47,9 +47,14 @@ KERNEL_SYMBOL = {
     "gemm_xstack_tangent": "chain_gemm_kernel<7, 4>", "gemm_block_tangent": "chain_gemm_kernel<7, 5>",
     "gemm_block_reverse": "chain_gemm_kernel<7, 6>", "tn_weight_grad": "tnw_kernel",
     "fused_fwd_inputgrad": "phaseA_kernel", "fused_tangent_reverse": "phaseC_kernel",
-    "rollout": "rollout_kernel", "grad_finalize": "slabsum_kernel",
+    "fused_phases_pipelined": ("phaseA_kernel", "phaseC_kernel"),
+    "rollout": "rollout_kernel", "grad_finalize": "tilefin_kernel",
 }
-MFMA_LAUNCHES = ("fused_fwd_inputgrad", "fused_tangent_reverse", "tn_weight_grad", "gemm_")
+# the profile records that time MFMA work.  fused_phases_pipelined is one
+# record per step for both phase kernels: two path chunks on two streams,
+# events around the whole section (its kernels overlap, so per-launch times
+# of a single kernel would not add up to the step)
+MFMA_LAUNCHES = ("fused_phases_pipelined", "fused_fwd_inputgrad", "fused_tangent_reverse", "tn_weight_grad", "gemm_")
 
 # BASELINE.json configs (the headline is "bsb")
 WORKLOADS = {
@@ -102,22 +107,32 @@ def cpu_baseline(iters=10, warmup=2):
 
 
 def traffic_from_pmc(symbol, launches_per_step):
-    """HBM bytes per launch of `symbol` from a committed rocprofv3 --pmc
-    counter collection (profiles/*pmc*counter_collection.csv): FETCH_SIZE is
-    doubled (gfx950 reports half of wide coalesced reads, MI355X_MICROARCH.md
-    HBM section), WRITE_SIZE taken as is; both counters are in KB."""
+    """HBM bytes per launch of `symbol` (or per record of a tuple of symbols:
+    the sum over them, each at its launches per record) from a committed
+    rocprofv3 --pmc counter collection (profiles/<round>_pmc*counter_collection.csv):
+    FETCH_SIZE is doubled (gfx950 reports half of wide coalesced reads,
+    MI355X_MICROARCH.md HBM section), WRITE_SIZE taken as is; both in KB.
+    The counter runs use the same bench command, so a kernel's launches per
+    step there equal the timed run's."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc*counter_collection.csv")))
     if not files:
         return None
-    sums = {"FETCH_SIZE": [], "WRITE_SIZE": []}
-    for f in files:
-        with open(f) as fh:
-            for row in csv.DictReader(fh):
-                if symbol in row.get("Kernel_Name", "") and row.get("Counter_Name") in sums:
-                    sums[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    if not sums["FETCH_SIZE"] or not sums["WRITE_SIZE"]:
-        return None
-    return 1024.0 * (2.0 * np.mean(sums["FETCH_SIZE"]) + np.mean(sums["WRITE_SIZE"]))
+    symbols = symbol if isinstance(symbol, tuple) else (symbol,)
+    total = 0.0
+    for sym in symbols:
+        sums = {"FETCH_SIZE": [], "WRITE_SIZE": []}
+        for f in files:
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if sym in row.get("Kernel_Name", "") and row.get("Counter_Name") in sums:
+                        sums[row["Counter_Name"]].append(float(row["Counter_Value"]))
+        if not sums["FETCH_SIZE"] or not sums["WRITE_SIZE"]:
+            return None
+        per_launch = 1024.0 * (2.0 * np.mean(sums["FETCH_SIZE"]) + np.mean(sums["WRITE_SIZE"]))
+        # launches of this symbol per record: the phase kernels run once per chunk
+        n = 2.0 if len(symbols) > 1 else 1.0
+        total += per_launch * n
+    return total
 
 
 def build_model(pkg, wl, M, dev, args):
@@ -238,10 +253,21 @@ def main():
     achieved = st["flops"] / st["launches"] / (avg_ms * 1e-3) / 1e12
     symbol = KERNEL_SYMBOL.get(name, name)
     traffic = traffic_from_pmc(symbol, st["launches"] / args.steps) if args.workload == "bsb" else None
+    symtxt = " + ".join(symbol) if isinstance(symbol, tuple) else symbol
     roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic, "kernel": f"{name} ({symbol})",
+                "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic, "kernel": f"{name} ({symtxt})",
                 "avg_launch_ms": avg_ms, "launches_per_step": st["launches"] / args.steps,
                 "alg_flops_per_launch": st["flops"] / st["launches"]}
+    # every other MFMA record, same definition (e.g. the weight-gradient kernel)
+    roofline_others = {}
+    for k, v in mfma.items():
+        if k == name:
+            continue
+        a_ms = v["ms"] / v["launches"]
+        a_tf = v["flops"] / v["launches"] / (a_ms * 1e-3) / 1e12
+        roofline_others[k] = {"achieved": a_tf, "frac": a_tf / PEAK_FP32_MFMA_TFLOPS, "avg_launch_ms": a_ms,
+                              "traffic": traffic_from_pmc(KERNEL_SYMBOL.get(k, k), 1.0)
+                              if args.workload == "bsb" else None}
     # the path-step kernel against HBM (north_star: achieved GB/s of the path step)
     rp = prof.get("rollout")
     roofline_path = None
@@ -278,6 +304,7 @@ def main():
                    "paths_per_gpu": Mloc, "global_batch": M_global, "time_steps": wl["N"],
                    "parallelism": f"dp{world}"},
         "roofline": roofline,
+        "roofline_other_mfma": roofline_others,
         "roofline_path_step": roofline_path,
         "allreduce_us": allreduce_us,
         "per_gpu_path_steps_per_s": value / world,

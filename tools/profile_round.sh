@@ -5,7 +5,7 @@
 # gpurun_out/prof_<tag>/; copy the summaries into profiles/ afterwards.
 #   tools/profile_round.sh <tag>
 set -o pipefail
-tag=${1:-r1}
+tag=${1:-r2}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 export TMPDIR=/tmp
