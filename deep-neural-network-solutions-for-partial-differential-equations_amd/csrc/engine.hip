@@ -139,6 +139,7 @@ struct dbsde_ctx {
 
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
+  bool x3 = false;                // ... in their split-bf16 form (phase.hpp)
   // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
   // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
   std::vector<float*> imgX, imgZ, imgF, imgB;
@@ -257,23 +258,28 @@ int join_side(dbsde_ctx* c, int i) {
 // ---------------------------------------------------------------------------
 // fused phase-kernel instantiations: (level tiles T, D tiles TD, blocks K)
 struct FusedVariant {
-  int T, TD, K, act, hv;
+  int T, TD, K, act, hv, x3;
   void (*A)(FusedArgs);
   void (*C)(FusedArgs);
 };
 // HV: the network has the NAIS x-stack (V_j); a template flag, so each kernel
-// carries only its own code path (smaller straight-line kernels)
-#define FV(T, TD, K, ACT, HV) {T, TD, K, ACT, HV, phaseA_kernel<T, TD, K, ACT, HV>, phaseC_kernel<T, TD, K, ACT, HV>}
-#define FV2(T, TD, K, ACT) FV(T, TD, K, ACT, true), FV(T, TD, K, ACT, false)
+// carries only its own code path (smaller straight-line kernels).  X3: the
+// split-bf16 matrix-core form (phase.hpp), at width 110/112; the fp32-input
+// MFMA form stays selectable (DBSDE_X3=0) and serves width 16.
+#define FV(T, TD, K, ACT, HV, X3) \
+  {T, TD, K, ACT, HV, X3, phaseA_kernel<T, TD, K, ACT, HV, X3>, phaseC_kernel<T, TD, K, ACT, HV, X3>}
+#define FV2(T, TD, K, ACT, X3) FV(T, TD, K, ACT, true, X3), FV(T, TD, K, ACT, false, X3)
 const FusedVariant kFused[] = {
-    FV2(7, 7, 3, 0), FV2(7, 7, 3, 1), FV2(7, 7, 3, 2), FV2(1, 1, 1, 0), FV2(1, 1, 1, 1), FV2(1, 1, 1, 2),
-    FV2(1, 1, 2, 0), FV2(1, 1, 2, 1), FV2(1, 1, 2, 2), FV2(1, 1, 3, 0), FV2(1, 1, 3, 1), FV2(1, 1, 3, 2),
+    FV2(7, 7, 3, 0, 1), FV2(7, 7, 3, 1, 1), FV2(7, 7, 3, 2, 1), FV2(7, 7, 3, 0, 0), FV2(7, 7, 3, 1, 0),
+    FV2(7, 7, 3, 2, 0), FV2(1, 1, 1, 0, 0), FV2(1, 1, 1, 1, 0), FV2(1, 1, 1, 2, 0), FV2(1, 1, 2, 0, 0),
+    FV2(1, 1, 2, 1, 0), FV2(1, 1, 2, 2, 0), FV2(1, 1, 3, 0, 0), FV2(1, 1, 3, 1, 0), FV2(1, 1, 3, 2, 0),
 };
 #undef FV2
 #undef FV
-int fused_variant(int T, int TD, int K, int act, bool hv) {
+int fused_variant(int T, int TD, int K, int act, bool hv, bool x3) {
   for (int i = 0; i < (int)(sizeof(kFused) / sizeof(kFused[0])); ++i)
-    if (kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv)
+    if (kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv &&
+        kFused[i].x3 == (int)x3)
       return i;
   return -1;
 }
@@ -373,7 +379,11 @@ int build_net(dbsde_ctx* c) {
   for (int j = 1; j <= c->K; ++j) uniform = uniform && c->Wp[j] == c->Wp[0];
   const char* env = getenv("DBSDE_FUSED");
   const bool allow = !(env && env[0] == '0');
-  c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v) >= 0;
+  const char* ex3 = getenv("DBSDE_X3");
+  const bool want_x3 = !(ex3 && ex3[0] == '0');
+  c->x3 = want_x3 && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, true) >= 0;
+  c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3) >= 0;
+  c->x3 = c->x3 && c->fused;
   // problem kind: Brownian dimension, g columns, u clamp
   const dbsde_problem& pr = g.problem;
   if (pr.kind != DBSDE_PROB_DIAG && pr.kind != DBSDE_PROB_HESTON) return fail(c, DBSDE_EINVAL, "unknown problem kind");
@@ -464,22 +474,29 @@ int build_buffers(dbsde_ctx* c) {
   c->imgZ.assign(K + 1, nullptr);
   c->imgF.assign(K + 1, nullptr);
   c->imgB.assign(K + 1, nullptr);
+  // floats of an image with tout output / tin input blocks of 16: fp32
+  // fragments (1 KiB each), or split-bf16 fragments (3 KiB per 32-wide block)
+  auto img_floats = [&](int tout, int tin) -> size_t {
+    return c->x3 ? (size_t)tout * ((tin + 1) / 2) * 768 : (size_t)tout * tin * 256;
+  };
   if (c->fused) {
     for (int j = 0; j <= (c->has_v ? K : 0); ++j) {
-      if ((rc = dalloc_t(c, &c->imgX[j], (size_t)TW * TDp * 256))) return rc;
-      if ((rc = dalloc_t(c, &c->imgZ[j], (size_t)TW * TDp * 256))) return rc;
+      if ((rc = dalloc_t(c, &c->imgX[j], img_floats(TW, TDp)))) return rc;
+      if ((rc = dalloc_t(c, &c->imgZ[j], img_floats(TDp, TW)))) return rc;
     }
     for (int j = 1; j <= K; ++j) {
-      if ((rc = dalloc_t(c, &c->imgF[j], (size_t)TW * TW * 256))) return rc;
-      if ((rc = dalloc_t(c, &c->imgB[j], (size_t)TW * TW * 256))) return rc;
+      if ((rc = dalloc_t(c, &c->imgF[j], img_floats(TW, TW)))) return rc;
+      if ((rc = dalloc_t(c, &c->imgB[j], img_floats(TW, TW)))) return rc;
     }
   }
-  auto frag = [](PackDesc d, float* img, int tin, int tout, int row0, int col0) {
+  const int fsplit = c->x3 ? 1 : 0;
+  auto frag = [fsplit](PackDesc d, float* img, int tin, int tout, int row0, int col0) {
     d.fdst = img;
     d.ftin = tin;
     d.ftout = tout;
     d.frow0 = row0;
     d.fcol0 = col0;
+    d.fsplit = fsplit;
     return d;
   };
 
@@ -853,7 +870,19 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
       d.dst[(size_t)r * d.dst_ld + cc] = v;
     if (d.fdst) {
       const int dr = (d.transpose ? cc : r) + d.frow0, dc = (d.transpose ? r : cc) + d.fcol0;
-      d.fdst[frag_off(dr, dc, d.ftin, d.ftout)] = v;
+      if (d.fsplit) {
+        // v = hi + mid + lo exactly (8 + 8 + 8 significand bits, truncating splits)
+        unsigned short* img = (unsigned short*)d.fdst + x3_off(dr, dc, d.ftout);
+        const unsigned u = __float_as_uint(v);
+        const float r1 = v - __uint_as_float(u & 0xffff0000u);
+        const unsigned u1 = __float_as_uint(r1);
+        const float r2 = r1 - __uint_as_float(u1 & 0xffff0000u);
+        img[0] = (unsigned short)(u >> 16);
+        img[512] = (unsigned short)(u1 >> 16);
+        img[1024] = (unsigned short)(__float_as_uint(r2) >> 16);
+      } else {
+        d.fdst[frag_off(dr, dc, d.ftin, d.ftout)] = v;
+      }
     }
   }
 }
@@ -1217,6 +1246,13 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
   // blocks [0, H) and [H, TI)
   const int TW = c->Wp[0] / 16, TDp = c->Dp / 16, K = c->K;
   auto add = [&](const float** imgs, int* nfs, int& n, const float* img, int TO, int TI) {
+    if (c->x3) {   // one piece per 32-wide input block: TO fragments of 3 chunks
+      for (int kb = 0; kb < (TI + 1) / 2; ++kb) {
+        imgs[n] = img + (size_t)kb * TO * 768;
+        nfs[n++] = 3 * TO;
+      }
+      return;
+    }
     if (TI < 2) {
       imgs[n] = img;
       nfs[n++] = TO * TI;
@@ -1378,7 +1414,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
 
   int nloss_parts;
   FusedArgs fa;
-  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act, c->has_v) : -1;
+  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act, c->has_v, c->x3) : -1;
   if (fv >= 0) {
     fa = fused_args(c, R, Rp, N1, q3);
     const int nv = nv_x(c);

@@ -44,11 +44,13 @@ struct FusedArgs {
   double* loss_part;        // [Rp / 64] per-workgroup loss sums
   float *Hdot, *Alpha;
   // fragment images of the stage sequence of each pass (phase.hpp)
-  const float* simgA[32];
-  int snfA[32];
+  // (fp32 images: two pieces per stage; split-bf16 images: one piece per
+  // 32-wide input block, phase.hpp)
+  const float* simgA[64];
+  int snfA[64];
   int nA;
-  const float* simgC[32];
-  int snfC[32];
+  const float* simgC[64];
+  int snfC[64];
   int nC;
 };
 

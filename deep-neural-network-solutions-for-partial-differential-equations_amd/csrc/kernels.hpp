@@ -620,9 +620,21 @@ struct PackDesc {
   // (dr, dc) = transpose ? (c, r) : (r, c); ftin = 16-col input blocks
   float* fdst;
   int ftin, frow0, fcol0;
-  int ftout;           // > 0: t-major image (phase3.hpp), fragment (o, t) at t * ftout + o
+  int ftout;           // > 0: t-major image (phase.hpp), fragment (o, t) at t * ftout + o
+  int fsplit;          // 1: split-bf16 image (x3_off), fdst holds bf16 triples
   int sp, sr0, sc0;    // tilefin_kernel: the window's problem tile and its first row / column
 };
+// bf16 offset of W[o][i] in a split-bf16 fragment image (phase.hpp, X3 kernels)
+// with tout 16-row output blocks: fragment (o/16, kb = i/32) at kb * tout + o/16,
+// 3 KiB = [hi | mid | lo] x 64 lanes x 8 bf16; lane (o%16) + 16 q, element j
+// for input column i = 32 kb + 16 (j >> 2) + 4 q + (j & 3) -- the permuted k
+// order in which a 16x16 MFMA output tile pair is already the next layer's
+// 16x16x32 B operand.  The mid / lo parts sit 512 / 1024 bf16 further on.
+__host__ __device__ __forceinline__ long long x3_off(int o, int i, int tout) {
+  const int ii = i & 31, q = (ii >> 2) & 3, j = ((ii >> 4) << 2) | (ii & 3);
+  const long long f = (long long)(i >> 5) * tout + (o >> 4);
+  return f * 1536 + ((o & 15) + 16 * q) * 8 + j;
+}
 // float offset of W[o][i] in a fragment image with tin input / tout output
 // blocks: fragment (o/16, i/16) -- o-major (phase.hpp) or, when tout > 0,
 // t-major (phase3.hpp) -- lane (o%16) + 16 ((i/4)%4), component i%4

@@ -226,12 +226,106 @@ struct NoOp {
   __device__ __forceinline__ void operator()() const {}
 };
 
-// one stage = one operand image: two pieces (one when TI == 1); `after` runs
-// right after the first piece's barrier (deferred stores, early loads).
+// ---------------------------------------------------------------------------
+// Split-bf16 products (X3 kernels).  An fp32 value is the exact sum of three
+// bf16 parts, x = hi + mid + lo (truncating splits: 8 + 8 + 8 significand
+// bits), and W x is accumulated as the six v_mfma_f32_16x16x32_bf16 products
+// Wl.xh + Wh.xl + Wm.xm + Wm.xh + Wh.xm + Wh.xh; the three dropped products
+// are below 2^-24 relative.  Every bf16 product is exact in the fp32
+// accumulator, so the result is as accurate as the fp32-input MFMA chain
+// (tools/ubench/x3_acc.hip on the GPU: mean error / sum|w x| 1.6e-8 against
+// 2.0e-8 for v_mfma_f32_16x16x4_f32, max 2.2e-7 against 2.3e-7) at 16/6 of its
+// rate on the matrix cores, which also leave the vector ALUs to the epilogues.
+// Operand order: a 32-wide input block kb is the pair of 16-column register
+// blocks (2 kb, 2 kb + 1) of the B-layout tile; lane (cl, q) element j holds
+// column 32 kb + 16 (j >> 2) + 4 q + (j & 3) -- no data movement between
+// layers, the weight image carries the same permutation (x3_off).
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+  bf16x8 h, m, l;
+};
+__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
+// [upper half of a | upper half of b << 16]: two truncated bf16 in one dword
+__device__ __forceinline__ unsigned hi_pair(float a, float b) {
+  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+template <int TI, int KB>
+__device__ __forceinline__ Split3 split_block(const Mat<TI>& b) {
+  float x[8], r1[8], r2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int t = 2 * KB + (j >> 2);
+    x[j] = t < TI ? b.v[t < TI ? t : 0][j & 3] : 0.f;
+    r1[j] = x[j] - trunc_bf16(x[j]);
+    r2[j] = r1[j] - trunc_bf16(r1[j]);
+  }
+  uintx4 H, M, L;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    H[d] = hi_pair(x[2 * d], x[2 * d + 1]);
+    M[d] = hi_pair(r1[2 * d], r1[2 * d + 1]);
+    L[d] = hi_pair(r2[2 * d], r2[2 * d + 1]);
+  }
+  return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, M), __builtin_bit_cast(bf16x8, L)};
+}
+__device__ __forceinline__ floatx4 mfma_bf(uintx4 a, const bf16x8& b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
+}
+// acc[o] += W(o, kb) . b(kb) over one piece = the TO fragments of input block
+// kb, fragment o at chunks 3 o .. 3 o + 2 (hi, mid, lo); the next fragment's
+// three ds_read_b128 are issued before this fragment's six MFMAs.
+template <int TO>
+__device__ __forceinline__ void sgemm_x3_piece(Mat<TO>& acc, const Split3& s, const floatx4* img, int lane) {
+  const uintx4* im = (const uintx4*)img;
+  uintx4 w[2][3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) w[0][p] = im[p * 64 + lane];
+#pragma unroll
+  for (int o = 0; o < TO; ++o) {
+    if (o + 1 < TO) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w[(o + 1) & 1][p] = im[(3 * (o + 1) + p) * 64 + lane];
+    }
+    const uintx4* wc = w[o & 1];
+    floatx4 a = acc.v[o];
+    a = mfma_bf(wc[2], s.h, a);
+    a = mfma_bf(wc[0], s.l, a);
+    a = mfma_bf(wc[1], s.m, a);
+    a = mfma_bf(wc[1], s.h, a);
+    a = mfma_bf(wc[0], s.m, a);
+    acc.v[o] = mfma_bf(wc[0], s.h, a);
+  }
+}
+template <int TO, int TI, int NPRE, int NAFTER, int KB, class F>
+__device__ __forceinline__ void stage_x3_from(Mat<TO>& acc, const Mat<TI>& b, PieceStager& sg, int lane, F&& after) {
+  constexpr int NKB = (TI + 1) / 2;
+  if constexpr (KB < NKB) {
+    const Split3 s = split_block<TI, KB>(b);
+    const floatx4* w = sg.template next<KB == 0 ? NPRE : (KB == 1 ? NAFTER : 0)>();
+    if constexpr (KB == 0) {
+      after();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    sgemm_x3_piece<TO>(acc, s, w, lane);
+    sg.mark();
+    stage_x3_from<TO, TI, NPRE, NAFTER, KB + 1>(acc, b, sg, lane, after);
+  }
+}
+
+// one stage = one operand image: two pieces (one when TI == 1), or in the X3
+// kernels one piece per 32-wide input block; `after` runs right after the
+// first piece's barrier (deferred stores, early loads).
 // NPRE = vector-memory ops issued since the first piece's DMA (the previous
 // stage's epilogue), NAFTER = the ops `after` issues (both lower bounds).
-template <int TO, int TI, int NPRE, int NAFTER, bool PF = false, class F>
+template <bool X3, int TO, int TI, int NPRE, int NAFTER, bool PF = false, class F>
 __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceStager& sg, int lane, F&& after) {
+  if constexpr (X3) {
+    stage_x3_from<TO, TI, NPRE, NAFTER, 0>(acc, b, sg, lane, after);
+    return;
+  }
   constexpr int H = (TI + 1) / 2;
   const floatx4* w = sg.template next<NPRE>();
   after();
@@ -256,10 +350,10 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceSt
 // phase A: forward + input gradient + Z (+ residual row sums)
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, {[Z_j], B_j} j=K..1, Z0
 // ---------------------------------------------------------------------------
-template <int T, int TD, int K, int ACT, bool HV>
+template <int T, int TD, int K, int ACT, bool HV, bool X3>
 __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   constexpr bool PFA = true;    // group-ahead fragment prefetch (sgemm_piece)
-  constexpr int TB = T > TD ? T : TD, BUF = ((TB + 1) / 2) * TB * 64;
+  constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[2 * BUF];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -274,7 +368,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   Mat<T> s1[K + 1];   // act'(a_j)
   Mat<T> h, acc;
   zero(acc);
-  stage_mm<T, TD, TD, 0, PFA>(acc, x, sg, lane, NoOp{});
+  stage_mm<X3, T, TD, TD, 0, PFA>(acc, x, sg, lane, NoOp{});
   fstore(acc, p.Abuf, S, row0, 0);
 #pragma unroll
   for (int o = 0; o < T; ++o)
@@ -288,8 +382,8 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero(acc);
-    stage_mm<T, T, T, T, PFA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd); });
-    if constexpr (HV) stage_mm<T, TD, 0, 0, PFA>(acc, x, sg, lane, NoOp{});
+    stage_mm<X3, T, T, T, T, PFA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd); });
+    if constexpr (HV) stage_mm<X3, T, TD, 0, 0, PFA>(acc, x, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o) {
       if constexpr (!HV) {
@@ -353,10 +447,10 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
     zero(gn);
     constexpr int NPREV = j < K ? 2 * T : T;
     if constexpr (HV) {
-      stage_mm<TD, T, 0, NPREV, PFA>(z, dl, sg, lane, prev);   // Z += delta_j V_j
-      stage_mm<T, T, 0, 0, PFA>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
+      stage_mm<X3, TD, T, 0, NPREV, PFA>(z, dl, sg, lane, prev);   // Z += delta_j V_j
+      stage_mm<X3, T, T, 0, 0, PFA>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
     } else {
-      stage_mm<T, T, 0, NPREV, PFA>(gn, dl, sg, lane, prev);
+      stage_mm<X3, T, T, 0, NPREV, PFA>(gn, dl, sg, lane, prev);
     }
 #pragma unroll
     for (int o = 0; o < T; ++o)
@@ -367,7 +461,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
         dl.v[o][r] = gv * s1[j - 1].v[o][r];
       }
   });
-  stage_mm<TD, T, 0, 2 * T + TD, PFA>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
+  stage_mm<X3, TD, T, 0, 2 * T + TD, PFA>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
     fstore(g, p.G, S, row0, 0);
     bstore_stream(dl, p.Delta, S, row0, 0);
     bload(x, p.xin, p.Dp, row0, 0);
@@ -420,7 +514,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
 // phase C: cotangents + forward tangent along zbar + reverse over (primal, tangent)
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, B_j j=K..1
 // ---------------------------------------------------------------------------
-template <int T, int TD, int K, int ACT, bool HV>
+template <int T, int TD, int K, int ACT, bool HV, bool X3>
 __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
 #ifndef DBSDE_PFC_T
 #define DBSDE_PFC_T true
@@ -429,7 +523,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
 #define DBSDE_PFC_R false
 #endif
   constexpr bool PFC_T = DBSDE_PFC_T, PFC_R = DBSDE_PFC_R;   // prefetch in the tangent / reverse stages
-  constexpr int TB = T > TD ? T : TD, BUF = ((TB + 1) / 2) * TB * 64;
+  constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[2 * BUF];
   __shared__ double lsum[P3_WAVES];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
@@ -486,7 +580,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   Mat<T> ad[K + 1];   // adot_j
   Mat<T> hd, av;
   zero(ad[0]);
-  stage_mm<T, TD, TD, T, PFC_T>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
+  stage_mm<X3, T, TD, TD, T, PFC_T>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
     fload(av, p.Abuf, S, row0, 0);
     if (threadIdx.x == 0) p.loss_part[tile] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
   });
@@ -497,11 +591,11 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero(ad[j]);
-    stage_mm<T, T, 0, 2 * T, PFC_T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
+    stage_mm<X3, T, T, 0, 2 * T, PFC_T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
       bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd);
       fload(av, p.Abuf, S, row0, j * Wd);
     });
-    if constexpr (HV) stage_mm<T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
+    if constexpr (HV) stage_mm<X3, T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
@@ -528,7 +622,7 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
     constexpr int j = K - decltype(ic)::value;
     Mat<T> acc, gg;
     zero(acc);
-    stage_mm<T, T, 0, 3 * T, PFC_R>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
+    stage_mm<X3, T, T, 0, 3 * T, PFC_R>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
       bstore_stream(al, p.Alpha, S, row0, j * Wd);
       fload(av, p.Abuf, S, row0, (j - 1) * Wd);
       fload(gg, p.G, S, row0, (j - 1) * Wd);

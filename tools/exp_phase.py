@@ -74,10 +74,20 @@ def edit(src, name):
             if "bstore(" in ln and "void bstore" not in ln and any(a in ln for a in nt_arrays):
                 lines[i] = ln.replace("bstore(", "bstore_nt(")
         src = "\n".join(lines)
-    if name in ("nostage", "bare"):
+    if name in ("nostoreall", "bareall"):   # every activation store (bstore, fstore, streaming) dropped
+        for fn in ("bstore", "fstore", "bstore_stream"):
+            sig = "__device__ __forceinline__ void %s(const Mat<TT>& m, float* base, int ld, int row0, int col0) {" % fn
+            assert sig in src, fn
+            src = src.replace(sig, sig + "\n  if (ld > 0) return;")
+    if name in ("noloadall", "bareall"):    # every activation load (bload, fload) returns zeros
+        for fn in ("bload", "fload"):
+            sig = "__device__ __forceinline__ void %s(Mat<TT>& m, const float* base, int ld, int row0, int col0) {" % fn
+            assert sig in src, fn
+            src = src.replace(sig, sig + "\n  if (ld > 0) { for (int t = 0; t < TT; ++t) m.v[t] = floatx4{0.f, 0.f, 0.f, 0.f}; return; }")
+    if name in ("nostage", "bare", "bareall"):
         src = src.replace("  __device__ __forceinline__ const floatx4* next() {\n",
                           "  __device__ __forceinline__ const floatx4* next() {\n"
-                          "    if (st++ > 0) return wl;\n    vm_wait0();\n    __syncthreads();\n    return wl;\n")
+                          "    if (st++ > 0) return wl;\n    vm_wait<0>();\n    __syncthreads();\n    return wl;\n")
     return src
 
 
