@@ -10,8 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 # translation units and their extra flags: the weight-gradient kernel is built
-# with VGPR-form MFMA (see csrc/tnw.hip); everything else with the defaults
-UNITS = [("engine.hip", []), ("evals.hip", []), ("tnw.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=true"])]
+# with VGPR-form MFMA (see csrc/tnw.hip); everything else (its split-bf16 form
+# tnwx3.hip included: accumulators in AGPRs) with the defaults
+UNITS = [("engine.hip", []), ("evals.hip", []), ("tnw.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]),
+         ("tnwx3.hip", [])]
 DEPS = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith((".hip", ".hpp"))] + \
     [os.path.join(ROOT, "include", "dbsde.h")]
 OUT = os.path.join(HERE, "lib", "libdbsde.so")

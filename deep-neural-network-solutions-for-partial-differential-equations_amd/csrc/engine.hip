@@ -147,6 +147,7 @@ struct dbsde_ctx {
   // wave-owned weight-gradient tiles (tnw.hpp): NAIS layouts with Dp == Wp
   bool tnw = false;
   int tnw_nb = 0, tnw_P = 0, tnw_S = 128;  // P * S = 1024 waves = one per SIMD at K = 3
+  bool tnw_x3 = false;                     // split-bf16 weight-gradient kernel (tnwx3.hip)
   float* slabW = nullptr;
   int fin_blocks = 1;             // slabsum grid.x
 
@@ -559,6 +560,8 @@ int build_buffers(dbsde_ctx* c) {
     const int T = Dp, P = 2 * K + 2, S = c->tnw_S;
     c->tnw_nb = T / 16;
     c->tnw_P = P;
+    const char* ex = getenv("DBSDE_TNW_X3");
+    c->tnw_x3 = c->x3 && c->tnw_nb == 7 && !(ex && ex[0] == '0');
     if (c->proj) {
       c->dot_nused = (T * T + TF_ELEMS - 1) / TF_ELEMS;
       if (c->dot_nused > c->dot_nblk) return fail(c, DBSDE_EINVAL, "internal: dot partials");
@@ -1050,7 +1053,12 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp) {
   hipStream_t s = c->stream;
   (void)grid;
   if (c->tnw_nb < 1 || c->tnw_nb > 8) return fail(c, DBSDE_EINVAL, "internal: tnw tile");
-  RUN(c, "tn_weight_grad", fl, 0.0, (void)tnw_launch(c->tnw_nb, a, s));
+  if (c->tnw_x3) {
+    if (Rp % 32 != 0) return fail(c, DBSDE_EINVAL, "internal: tnw x3 geometry");
+    RUN(c, "tn_weight_grad", fl, 0.0, (void)tnw_x3_launch(c->tnw_nb, a, s));
+  } else {
+    RUN(c, "tn_weight_grad", fl, 0.0, (void)tnw_launch(c->tnw_nb, a, s));
+  }
   return DBSDE_OK;
 }
 

@@ -168,21 +168,31 @@ __device__ __forceinline__ void piece_dma(const float* img, int nf, floatx4* buf
   for (int f = wave; f < nf; f += P3_WAVES) glds16(img + (size_t)f * 256 + lane * 4, buf + f * 64);
 }
 
-// piece sequencer: wait for this piece, publish it, start the next one.
+// piece sequencer: wait for this piece, publish it, start the one NBUF - 1
+// ahead (NBUF-buffer LDS ring; the fp32 kernels use 2, the split-bf16 kernels,
+// whose pieces carry 1/4 of the MFMA work, 3).
 // NYOUNG = vector-memory operations this wave is guaranteed to have issued
 // after the piece's DMA (deferred stores, early loads): they may stay in flight
-// across the barrier.  Under-counting is safe, over-counting is a race.
-struct PieceStager {
+// across the barrier.  Under-counting is safe, over-counting is a race.  With
+// NBUF = 3 the DMA of the following piece was also issued after this piece's:
+// LC = a lower bound of this wave's chunks of it (waves copy 5 or 6 of 21).
+template <int NBUF, int LC>
+struct PieceStagerT {
   floatx4* wl;
   const float* const* img;
   const int* nf;
   int n, st, wave, lane, buf;
 #ifdef DBSDE_STAMPS   // diagnostic build (tools/exp_phase.py stamps): per-piece s_memtime
-  unsigned long long ts[3 * 32];
+  unsigned long long ts[3 * 64];
   __device__ __forceinline__ void mark() { ts[3 * (st - 1) + 2] = __builtin_amdgcn_s_memtime(); }
 #else
   __device__ __forceinline__ void mark() {}
 #endif
+  __device__ __forceinline__ void start() {
+#pragma unroll
+    for (int k = 0; k < NBUF - 1; ++k)
+      if (k < n) piece_dma(img[k], nf[k], wl + k * buf, wave, lane);
+  }
   template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
 #if defined(DBSDE_PRIO_EPI)
@@ -193,22 +203,34 @@ struct PieceStager {
 #ifdef DBSDE_STAMPS
     ts[3 * st] = __builtin_amdgcn_s_memtime();
 #endif
-    vm_wait<NYOUNG>();
+    if constexpr (NBUF > 2) {
+      if (st + 1 < n)
+        vm_wait<NYOUNG + LC>();
+      else
+        vm_wait<NYOUNG>();
+    } else {
+      vm_wait<NYOUNG>();
+    }
     lds_barrier();
 #ifdef DBSDE_STAMPS
     ts[3 * st + 1] = __builtin_amdgcn_s_memtime();
 #endif
-    if (st + 1 < n) piece_dma(img[st + 1], nf[st + 1], wl + ((st + 1) & 1) * buf, wave, lane);
+    constexpr int DIST = NBUF - 1;
+    if (st + DIST < n) piece_dma(img[st + DIST], nf[st + DIST], wl + ((st + DIST) % NBUF) * buf, wave, lane);
     // nothing issued later may be hoisted above the DMA (the NYOUNG counts)
     __builtin_amdgcn_sched_barrier(0);
-    const floatx4* cur = wl + (st & 1) * buf;
+    const floatx4* cur = wl + (st % NBUF) * buf;
     ++st;
     return cur;
   }
 };
+// the kernels' stager: X3 pieces are 3 TO chunks, TO >= min(T, TD)
+template <bool X3, int T, int TD>
+using PieceStager = PieceStagerT<X3 ? 3 : 2, X3 ? (3 * (T < TD ? T : TD)) / P3_WAVES : 0>;
 
 #ifdef DBSDE_STAMPS
-__device__ __forceinline__ void stamp_dump(const PieceStager& sg, char kind, int tile) {
+template <class SG>
+__device__ __forceinline__ void stamp_dump(const SG& sg, char kind, int tile) {
   const unsigned long long tend = __builtin_amdgcn_s_memtime();
   if ((tile == 5 || tile == 405 || tile == 805) && (threadIdx.x & 63) == 0)
     for (int i = 0; i < sg.n; ++i) {
@@ -274,22 +296,51 @@ __device__ __forceinline__ Split3 split_block(const Mat<TI>& b) {
 __device__ __forceinline__ floatx4 mfma_bf(uintx4 a, const bf16x8& b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
 }
+// split pair d (elements 2d, 2d + 1) of input block KB into dword d of the
+// hi / mid / lo operands
+template <int TI, int KB, int d>
+__device__ __forceinline__ void split_pair(const Mat<TI>& b, uintx4& H, uintx4& M, uintx4& L) {
+  float x[2], r1[2], r2[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int j = 2 * d + e, t = 2 * KB + (j >> 2);
+    x[e] = t < TI ? b.v[t < TI ? t : 0][j & 3] : 0.f;
+    r1[e] = x[e] - trunc_bf16(x[e]);
+    r2[e] = r1[e] - trunc_bf16(r1[e]);
+  }
+  H[d] = hi_pair(x[0], x[1]);
+  M[d] = hi_pair(r1[0], r1[1]);
+  L[d] = hi_pair(r2[0], r2[1]);
+}
 // acc[o] += W(o, kb) . b(kb) over one piece = the TO fragments of input block
-// kb, fragment o at chunks 3 o .. 3 o + 2 (hi, mid, lo); the next fragment's
-// three ds_read_b128 are issued before this fragment's six MFMAs.
-template <int TO>
-__device__ __forceinline__ void sgemm_x3_piece(Mat<TO>& acc, const Split3& s, const floatx4* img, int lane) {
+// kb, fragment o at chunks 3 o .. 3 o + 2 (hi, mid, lo).  Each fragment is one
+// scheduling region: the next fragment's three ds_read_b128 first, then its six
+// MFMAs with the split of the NEXT input block (KBN, one dword pair per
+// fragment) interleaved two VALU per MFMA gap -- the LDS latency and the split
+// hide under the matrix pipe.
+//   PF = false (register-tight stages): a fragment's reads open its own region.
+template <int TO, int TI, int KBN, bool PF>
+__device__ __forceinline__ void sgemm_x3_piece(Mat<TO>& acc, const Split3& s, const floatx4* img, int lane,
+                                               const Mat<TI>& b, uintx4 (&sn)[3]) {
+  constexpr bool NEXT = KBN < (TI + 1) / 2;
   const uintx4* im = (const uintx4*)img;
-  uintx4 w[2][3];
+  uintx4 w[PF ? 2 : 1][3];
+  if constexpr (PF) {
 #pragma unroll
-  for (int p = 0; p < 3; ++p) w[0][p] = im[p * 64 + lane];
-#pragma unroll
-  for (int o = 0; o < TO; ++o) {
-    if (o + 1 < TO) {
+    for (int p = 0; p < 3; ++p) w[0][p] = im[p * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  SFor<0, TO>::run([&](auto oc) __attribute__((always_inline)) {
+    constexpr int o = decltype(oc)::value;
+    if constexpr (PF && o + 1 < TO) {
 #pragma unroll
       for (int p = 0; p < 3; ++p) w[(o + 1) & 1][p] = im[(3 * (o + 1) + p) * 64 + lane];
+    } else if constexpr (!PF) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w[0][p] = im[(3 * o + p) * 64 + lane];
     }
-    const uintx4* wc = w[o & 1];
+    if constexpr (NEXT && o < 4) split_pair<TI, NEXT ? KBN : 0, o>(b, sn[0], sn[1], sn[2]);
+    const uintx4* wc = w[PF ? (o & 1) : 0];
     floatx4 a = acc.v[o];
     a = mfma_bf(wc[2], s.h, a);
     a = mfma_bf(wc[0], s.l, a);
@@ -297,21 +348,32 @@ __device__ __forceinline__ void sgemm_x3_piece(Mat<TO>& acc, const Split3& s, co
     a = mfma_bf(wc[1], s.h, a);
     a = mfma_bf(wc[0], s.m, a);
     acc.v[o] = mfma_bf(wc[0], s.h, a);
-  }
+    if constexpr (!PF || o + 1 < TO) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS read
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  });
 }
-template <int TO, int TI, int NPRE, int NAFTER, int KB, class F>
-__device__ __forceinline__ void stage_x3_from(Mat<TO>& acc, const Mat<TI>& b, PieceStager& sg, int lane, F&& after) {
+template <int TO, int TI, int NPRE, int NAFTER, int KB, bool PF, class SG, class F>
+__device__ __forceinline__ void stage_x3_from(Mat<TO>& acc, const Mat<TI>& b, SG& sg, int lane, F&& after,
+                                              const Split3& s) {
   constexpr int NKB = (TI + 1) / 2;
   if constexpr (KB < NKB) {
-    const Split3 s = split_block<TI, KB>(b);
     const floatx4* w = sg.template next<KB == 0 ? NPRE : (KB == 1 ? NAFTER : 0)>();
     if constexpr (KB == 0) {
       after();
       __builtin_amdgcn_sched_barrier(0);
     }
-    sgemm_x3_piece<TO>(acc, s, w, lane);
+    uintx4 sn[3];
+    sgemm_x3_piece<TO, TI, KB + 1, PF>(acc, s, w, lane, b, sn);
     sg.mark();
-    stage_x3_from<TO, TI, NPRE, NAFTER, KB + 1>(acc, b, sg, lane, after);
+    if constexpr (KB + 1 < NKB)
+      stage_x3_from<TO, TI, NPRE, NAFTER, KB + 1, PF>(
+          acc, b, sg, lane, after,
+          Split3{__builtin_bit_cast(bf16x8, sn[0]), __builtin_bit_cast(bf16x8, sn[1]), __builtin_bit_cast(bf16x8, sn[2])});
   }
 }
 
@@ -320,10 +382,10 @@ __device__ __forceinline__ void stage_x3_from(Mat<TO>& acc, const Mat<TI>& b, Pi
 // first piece's barrier (deferred stores, early loads).
 // NPRE = vector-memory ops issued since the first piece's DMA (the previous
 // stage's epilogue), NAFTER = the ops `after` issues (both lower bounds).
-template <bool X3, int TO, int TI, int NPRE, int NAFTER, bool PF = false, class F>
-__device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, PieceStager& sg, int lane, F&& after) {
+template <bool X3, int TO, int TI, int NPRE, int NAFTER, bool PF = false, class SG, class F>
+__device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, SG& sg, int lane, F&& after) {
   if constexpr (X3) {
-    stage_x3_from<TO, TI, NPRE, NAFTER, 0>(acc, b, sg, lane, after);
+    stage_x3_from<TO, TI, NPRE, NAFTER, 0, PF>(acc, b, sg, lane, after, split_block<TI, 0>(b));
     return;
   }
   constexpr int H = (TI + 1) / 2;
@@ -354,14 +416,14 @@ template <int T, int TD, int K, int ACT, bool HV, bool X3>
 __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
   constexpr bool PFA = true;    // group-ahead fragment prefetch (sgemm_piece)
   constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
-  __shared__ floatx4 wl[2 * BUF];
+  __shared__ floatx4 wl[(X3 ? 3 : 2) * BUF];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = blockIdx.x + p.tile0;   // 64-row tile (chunked launches offset it)
   const int row0 = tile * P3_ROWS + wave * 16;
   const int S = p.S, Wd = p.W;
-  PieceStager sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
-  piece_dma(p.simgA[0], p.snfA[0], wl, wave, lane);
+  PieceStager<X3, T, TD> sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
+  sg.start();
   Mat<TD> x;
   bload(x, p.xin, p.Dp, row0, 0);
 
@@ -522,17 +584,19 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
 #ifndef DBSDE_PFC_R
 #define DBSDE_PFC_R false
 #endif
-  constexpr bool PFC_T = DBSDE_PFC_T, PFC_R = DBSDE_PFC_R;   // prefetch in the tangent / reverse stages
+  // prefetch in the tangent / reverse stages (the split-bf16 form is at the
+  // register limit without it)
+  constexpr bool PFC_T = X3 ? false : DBSDE_PFC_T, PFC_R = X3 ? false : DBSDE_PFC_R;
   constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
-  __shared__ floatx4 wl[2 * BUF];
+  __shared__ floatx4 wl[(X3 ? 3 : 2) * BUF];
   __shared__ double lsum[P3_WAVES];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = blockIdx.x + p.tile0;   // 64-row tile (chunked launches offset it)
   const int row0 = tile * P3_ROWS + wave * 16;
   const int S = p.S, Wd = p.W;
-  PieceStager sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
-  piece_dma(p.simgC[0], p.snfC[0], wl, wave, lane);
+  PieceStager<X3, T, TD> sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
+  sg.start();
 
   // ---- residuals and closed-form cotangents of row cl (every lane of the row
   // computes them; the zbar columns 16 o + 4 q + r are this lane's)

@@ -53,5 +53,51 @@ struct TNWArgs {
 // three-stage operand ring fit one register class).  Returns -1 for an
 // unsupported nb; launch errors are left for hipGetLastError.
 __attribute__((visibility("hidden"))) int tnw_launch(int nb, const TNWArgs& a, hipStream_t s);
+// The same contraction in split-bf16 products (tnwx3.hip, 32-row k-steps; the
+// row slices are whole 32-row steps).  nb = 7 only; -1 otherwise.
+__attribute__((visibility("hidden"))) int tnw_x3_launch(int nb, const TNWArgs& a, hipStream_t s);
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// Output layer [w_out | b_out]: sum_r ubar_r h_r + hdot_r (and sum_r ubar_r)
+// as a one-block-row product whose A operand [ubar | 1 | 0 ...] is formed in
+// registers; row 0 of the tile is w_out, element (1, 0) is b_out.
+template <int NB>
+__device__ __forceinline__ void tnw_output(const TNWArgs& a, int g0, int g1, int i, int kq, float* out) {
+  floatx4 acc[NB];
+#pragma unroll
+  for (int n = 0; n < NB; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float bs = 0.f;
+#pragma unroll 4
+  for (int g = g0; g < g1; ++g) {
+    const int row = 4 * g + kq;
+    const float ub = a.ubar[row];
+    const float a1 = i == 0 ? ub : 0.f;
+    const float a2 = (i == 0 && row < a.R) ? 1.f : 0.f;
+    const float* h = a.Hk + (size_t)row * a.ldh + i;
+    const float* hd = a.Hdk + (size_t)row * a.ldh + i;
+    float b1[NB], b2[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      b1[n] = h[16 * n];
+      b2[n] = hd[16 * n];
+    }
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1[n], acc[n], 0, 0, 0);
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, b2[n], acc[n], 0, 0, 0);
+    }
+    bs += a1;
+  }
+  constexpr int T = 16 * NB;
+#pragma unroll
+  for (int n = 0; n < NB; ++n)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) out[(size_t)(4 * kq + v) * T + 16 * n + i] = acc[n][v];
+  // b_out partial: lanes 0, 16, 32, 48 hold the sums of their k rows
+  const float b = (__shfl(bs, 0) + __shfl(bs, 16)) + (__shfl(bs, 32) + __shfl(bs, 48));
+  if ((threadIdx.x & 63) == 0) out[T] = b;
+}
+
 
 }  // namespace dbsde

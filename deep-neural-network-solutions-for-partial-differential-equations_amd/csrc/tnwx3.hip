@@ -1,0 +1,137 @@
+// tnwx3.hip -- the wave-owned weight-gradient contraction (tnw.hpp) in
+// split-bf16 products.
+//
+// Each operand value is the exact sum of three bf16 parts (hi + mid + lo,
+// truncating splits, see phase.hpp) and every 16x16 output block accumulates
+// the six v_mfma_f32_16x16x32_bf16 products al.bh + ah.bl + am.bm + am.bh +
+// ah.bm + ah.bh over a 32-row k-step; the dropped products are below 2^-24
+// relative, so the sums are as accurate as the fp32-input MFMA chain of
+// tnw.hip (tools/ubench/x3_acc.hip) at 16/6 of its matrix rate.
+//
+// Operand layout of a 32-row step: lane (i, q) holds rows 8q .. 8q + 7 of
+// column 16m + i of A (the A operand A^T[16m + i][row]) and of column 16n + i
+// of B, eight dword loads per block.  One wave per SIMD (a 1024-wave grid):
+// the 7x7 accumulator tile sits in AGPRs (this unit is built with the default
+// MFMA register form), the split B operands of the step (84 VGPRs), the raw
+// next step (112) and one split A block in VGPRs; the next step's loads are
+// issued a whole step (294 MFMAs) ahead.
+#include "tnw.hpp"
+
+namespace dbsde {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+  bf16x8 h, m, l;
+};
+
+__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
+__device__ __forceinline__ unsigned hi_pair(float a, float b) {
+  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+__device__ __forceinline__ Split3 split8(const float (&x)[8]) {
+  uintx4 H, M, L;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const float x0 = x[2 * d], x1 = x[2 * d + 1];
+    const float r0 = x0 - trunc_bf16(x0), r1 = x1 - trunc_bf16(x1);
+    const float s0 = r0 - trunc_bf16(r0), s1 = r1 - trunc_bf16(r1);
+    H[d] = hi_pair(x0, x1);
+    M[d] = hi_pair(r0, r1);
+    L[d] = hi_pair(s0, s1);
+  }
+  return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, M), __builtin_bit_cast(bf16x8, L)};
+}
+__device__ __forceinline__ floatx4 mfma_bf(const bf16x8& a, const bf16x8& b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int NB>
+__device__ __forceinline__ void load_cols(float (&r)[NB][8], const float* X, int ld, int row0, int i) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float* p = X + (size_t)(row0 + j) * ld + i;
+#pragma unroll
+    for (int m = 0; m < NB; ++m) r[m][j] = p[16 * m];
+  }
+}
+
+// acc += A[rows]^T B[rows] over 32-row steps [g0, g1)
+template <int NB>
+__device__ __forceinline__ void x3_product(floatx4 (&acc)[NB][NB], const float* A, int lda, const float* B, int ldb,
+                                           int g0, int g1, int i, int q) {
+  float ra[NB][8], rb[NB][8];
+  load_cols<NB>(ra, A, lda, 32 * g0 + 8 * q, i);
+  load_cols<NB>(rb, B, ldb, 32 * g0 + 8 * q, i);
+  for (int g = g0; g < g1; ++g) {
+    const int nrow = 32 * min(g + 1, g1 - 1) + 8 * q;   // clamped prefetch, unused past the slice
+    Split3 sb[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) sb[n] = split8(rb[n]);
+    load_cols<NB>(rb, B, ldb, nrow, i);
+#pragma unroll
+    for (int m = 0; m < NB; ++m) {
+      const Split3 sa = split8(ra[m]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ra[m][j] = A[(size_t)(nrow + j) * lda + 16 * m + i];
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        floatx4 c = acc[m][n];
+        c = mfma_bf(sa.l, sb[n].h, c);
+        c = mfma_bf(sa.h, sb[n].l, c);
+        c = mfma_bf(sa.m, sb[n].m, c);
+        c = mfma_bf(sa.m, sb[n].h, c);
+        c = mfma_bf(sa.h, sb[n].m, c);
+        acc[m][n] = mfma_bf(sa.h, sb[n].h, c);
+      }
+    }
+  }
+}
+
+// the grid and problem / slice mapping of tnw_kernel (tnw.hip); slices are
+// whole 32-row steps
+template <int NB>
+__global__ void __launch_bounds__(256, 1) tnw_x3_kernel(TNWArgs a) {
+  const int wg = blockIdx.x, wpg = a.P / 4;
+  const int xcd = wg & 7, local = wg >> 3;
+  const int s = (local / wpg) * 8 + xcd;
+  const int p = (local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6);
+  const TNWProb& pr = a.prob[p];
+  const int lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
+  const int n32 = a.nchunk / 2;
+  const int c0 = (int)((long long)s * n32 / a.S), c1 = (int)((long long)(s + 1) * n32 / a.S);
+  constexpr int T = 16 * NB;
+  float* out = a.slab + ((size_t)s * a.P + p) * T * T;
+  if (p == a.P - 1) {
+    tnw_output<NB>(a, 8 * c0, 8 * c1, i, q, out);
+    return;
+  }
+  floatx4 acc[NB][NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (c1 > c0) {
+    x3_product<NB>(acc, pr.A1, pr.lda1, pr.B1, pr.ldb1, c0, c1, i, q);
+    x3_product<NB>(acc, pr.A2, pr.lda2, pr.B2, pr.ldb2, c0, c1, i, q);
+  }
+#pragma unroll
+  for (int m = 0; m < NB; ++m)
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) out[(size_t)(16 * m + 4 * q + v) * T + 16 * n + i] = acc[m][n][v];
+}
+
+}  // namespace
+
+int tnw_x3_launch(int nb, const TNWArgs& a, hipStream_t s) {
+  if (nb != 7 || a.nchunk % 2 != 0) return -1;
+  tnw_x3_kernel<7><<<(unsigned)(a.S * a.P / 4), 256, 0, s>>>(a);
+  return 0;
+}
+
+}  // namespace dbsde
