@@ -38,6 +38,11 @@ LAYERS = [D + 1] + 4 * [W_HID] + [1]
 LR = 1e-3
 U0_EXACT = float(np.exp((0.05 + 0.4 ** 2) * 1.0) * 62.5)     # DeepBSDE.py:345-349 at Xi=[1,.5]*50
 PEAK_FP32_MFMA_TFLOPS = 157.3                                # MI355X_MICROARCH.md, dense f32 MFMA
+# split-bf16 kernels (solver.matrix_form): an fp32 product block costs six dense
+# bf16 MFMAs, so their fp32-equivalent matrix peak is the dense bf16 peak / 6
+PEAK_BF16_DENSE_TFLOPS = 2500.0
+PEAK_X3_TFLOPS = PEAK_BF16_DENSE_TFLOPS / 6.0
+X3_RECORDS = {1: ("fused_phases_pipelined", "fused_fwd_inputgrad", "fused_tangent_reverse"), 2: ("tn_weight_grad",)}
 PEAK_HBM_GBS = 8000.0
 PROFILE_ROUND = "r2"          # profiles/<round>_pmc_* counter collections of the current build
 # rocprof symbol of each profiled launch class (EPI ids from csrc/kernels.hpp)
@@ -50,6 +55,7 @@ KERNEL_SYMBOL = {
     "fused_phases_pipelined": ("phaseA_kernel", "phaseC_kernel"),
     "rollout": "rollout_kernel", "grad_finalize": "tilefin_kernel",
 }
+KERNEL_SYMBOL_X3 = {"tn_weight_grad": "tnw_x3_kernel"}   # when matrix_form bit 1 is set
 # the profile records that time MFMA work.  fused_phases_pipelined is one
 # record per step for both phase kernels: two path chunks on two streams,
 # events around the whole section (its kernels overlap, so per-launch times
@@ -249,13 +255,31 @@ def main():
     # side-stream launches such as loss_final include queue wait in their events)
     mfma = {k: v for k, v in prof.items() if k.startswith(MFMA_LAUNCHES)}
     name, st = max(mfma.items(), key=lambda kv: kv[1]["ms"])
+    form = model.solver.matrix_form
+
+    def peak_of(rec):
+        """(peak, form text) of a record's matrix instruction: the split-bf16
+        kernels against the bf16 dense peak / 6 (fp32-equivalent FLOPs), the
+        fp32-input MFMA kernels against the fp32 MFMA peak"""
+        for bit, recs in X3_RECORDS.items():
+            if form & bit and rec.startswith(recs):
+                return PEAK_X3_TFLOPS, "split-bf16 (6 x v_mfma_f32_16x16x32_bf16 per fp32 block, fp32-accurate)"
+        return PEAK_FP32_MFMA_TFLOPS, "fp32-input MFMA (v_mfma_f32_16x16x4_f32)"
+
+    def sym_of(rec):
+        if form & 2 and rec in KERNEL_SYMBOL_X3:
+            return KERNEL_SYMBOL_X3[rec]
+        return KERNEL_SYMBOL.get(rec, rec)
+
     avg_ms = st["ms"] / st["launches"]
     achieved = st["flops"] / st["launches"] / (avg_ms * 1e-3) / 1e12
-    symbol = KERNEL_SYMBOL.get(name, name)
+    symbol = sym_of(name)
     traffic = traffic_from_pmc(symbol, st["launches"] / args.steps) if args.workload == "bsb" else None
     symtxt = " + ".join(symbol) if isinstance(symbol, tuple) else symbol
-    roofline = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic, "kernel": f"{name} ({symtxt})",
+    peak, form_txt = peak_of(name)
+    roofline = {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": achieved / peak, "traffic": traffic, "kernel": f"{name} ({symtxt})",
+                "matrix_form": form_txt, "frac_of_fp32_mfma_peak": achieved / PEAK_FP32_MFMA_TFLOPS,
                 "avg_launch_ms": avg_ms, "launches_per_step": st["launches"] / args.steps,
                 "alg_flops_per_launch": st["flops"] / st["launches"]}
     # every other MFMA record, same definition (e.g. the weight-gradient kernel)
@@ -265,8 +289,10 @@ def main():
             continue
         a_ms = v["ms"] / v["launches"]
         a_tf = v["flops"] / v["launches"] / (a_ms * 1e-3) / 1e12
-        roofline_others[k] = {"achieved": a_tf, "frac": a_tf / PEAK_FP32_MFMA_TFLOPS, "avg_launch_ms": a_ms,
-                              "traffic": traffic_from_pmc(KERNEL_SYMBOL.get(k, k), 1.0)
+        pk, ftxt = peak_of(k)
+        roofline_others[k] = {"achieved": a_tf, "peak": pk, "frac": a_tf / pk, "matrix_form": ftxt,
+                              "avg_launch_ms": a_ms,
+                              "traffic": traffic_from_pmc(sym_of(k), 1.0)
                               if args.workload == "bsb" else None}
     # the path-step kernel against HBM (north_star: achieved GB/s of the path step)
     rp = prof.get("rollout")

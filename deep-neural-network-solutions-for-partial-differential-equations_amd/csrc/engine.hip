@@ -1302,6 +1302,11 @@ extern "C" {
 
 int dbsde_abi_version(void) { return DBSDE_ABI_VERSION; }
 
+int dbsde_matrix_form(const dbsde_ctx* c) {
+  if (!c) return 0;
+  return (c->x3 ? 1 : 0) | (c->tnw && c->tnw_x3 ? 2 : 0);
+}
+
 const char* dbsde_last_error(const dbsde_ctx* ctx) {
   if (ctx && !ctx->err.empty()) return ctx->err.c_str();
   return g_last_error.c_str();

@@ -68,15 +68,21 @@ __device__ __forceinline__ void x3_product(floatx4 (&acc)[NB][NB], const float* 
   load_cols<NB>(rb, B, ldb, 32 * g0 + 8 * q, i);
   for (int g = g0; g < g1; ++g) {
     const int nrow = 32 * min(g + 1, g1 - 1) + 8 * q;   // clamped prefetch, unused past the slice
+    // pinned regions (sched_barrier): left alone, the scheduler sinks the
+    // next step's loads to the top of the next trip, right before their use
     Split3 sb[NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) sb[n] = split8(rb[n]);
+    __builtin_amdgcn_sched_barrier(0);
     load_cols<NB>(rb, B, ldb, nrow, i);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int m = 0; m < NB; ++m) {
       const Split3 sa = split8(ra[m]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) ra[m][j] = A[(size_t)(nrow + j) * lda + 16 * m + i];
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         floatx4 c = acc[m][n];
@@ -87,6 +93,7 @@ __device__ __forceinline__ void x3_product(floatx4 (&acc)[NB][NB], const float* 
         c = mfma_bf(sa.h, sb[n].m, c);
         acc[m][n] = mfma_bf(sa.h, sb[n].h, c);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }

@@ -90,6 +90,8 @@ class NativeSolver:
         _lib.check(self.lib.dbsde_param_used_mask(ctx, mask, self.nparams), ctx)
         self.used_mask = torch.frombuffer(bytearray(mask), dtype=torch.uint8).bool()
         self.nb = int(self.lib.dbsde_brownian_dim(ctx))
+        # bit 0: phase kernels, bit 1: weight-gradient kernel in split-bf16 form
+        self.matrix_form = int(self.lib.dbsde_matrix_form(ctx))
 
     def __del__(self):
         ctx = getattr(self, "ctx", None)

@@ -57,12 +57,15 @@ def dev():
     return torch.device("cuda:0")
 
 
-def make_solver(pkg, dev, g, fused=True, tnw=True):
+def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True):
     """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at
-    create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0)."""
+    create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0); x3=False
+    the fp32-input MFMA form of the fused phase and weight-gradient kernels
+    (DBSDE_X3=0 / DBSDE_TNW_X3=0) instead of the split-bf16 one."""
     layers = [int(v) for v in g["layers"]]
     D = layers[0] - 1
-    env = {"DBSDE_FUSED": "1" if fused else "0", "DBSDE_TNW": "1" if tnw else "0"}
+    env = {"DBSDE_FUSED": "1" if fused else "0", "DBSDE_TNW": "1" if tnw else "0",
+           "DBSDE_X3": "1" if x3 else "0", "DBSDE_TNW_X3": "1" if x3 else "0"}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -76,10 +79,10 @@ def make_solver(pkg, dev, g, fused=True, tnw=True):
                 os.environ[k] = v
 
 
-def native_case(pkg, dev, g, want_grad=True, fused=True):
+def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True):
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
-    s = make_solver(pkg, dev, g, fused)
+    s = make_solver(pkg, dev, g, fused, x3=x3)
     params = torch.from_numpy(g["params"]).to(dev)
     out = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (N + 1) * D, device=dev),
                Y=torch.empty(M * (N + 1), device=dev), Z=torch.empty(M * (N + 1) * D, device=dev))
@@ -98,11 +101,14 @@ def native_case(pkg, dev, g, want_grad=True, fused=True):
     return res
 
 
-@pytest.mark.parametrize("fused", [True, False], ids=["fused", "chain"])
+@pytest.mark.parametrize("fused", ["fused", "fused_fp32", "chain"])
 @pytest.mark.parametrize("path", G1, ids=[os.path.basename(p)[3:-4] for p in G1])
 def test_loss_grad_matches_reference(pkg, dev, path, fused):
+    """fused: the default fused kernels (split-bf16 matrix form at width
+    110/112); fused_fp32: the same kernels on fp32-input MFMA; chain: the
+    per-layer GEMM path."""
     g = _load(path)
-    r = native_case(pkg, dev, g, fused=fused)
+    r = native_case(pkg, dev, g, fused=fused != "chain", x3=fused == "fused")
     if str(g["problem"]) == "heston":
         # the reference's torch.sqrt on the CPU is MKL vsSqrt (ATen vml), which
         # is not correctly rounded at near-ties; the kernel's sqrt is (as numpy's,
@@ -262,7 +268,8 @@ def test_net_u_matches_fixture_Y(pkg, dev):
     np.testing.assert_allclose(du.cpu().numpy(), g["Z"].reshape(R, D), rtol=0, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False)], ids=["chain", "splitk_weight_grad"])
+@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False), dict(x3=False)],
+                         ids=["chain", "splitk_weight_grad", "fp32_mfma"])
 def test_kernel_paths_agree_at_north_star(pkg, dev, variant):
     """The default kernels (fused phases + wave-owned weight-gradient tiles)
     against the per-layer chain path and against the split-K weight-gradient
@@ -287,3 +294,35 @@ def test_kernel_paths_agree_at_north_star(pkg, dev, variant):
     assert abs(l1 - l2) <= 1e-5 * abs(l2)
     np.testing.assert_allclose(y1, y2, rtol=0, atol=1e-4)
     np.testing.assert_allclose(g1, g2, rtol=0, atol=1e-4 * np.abs(g2).max())
+
+
+def test_split_bf16_error_not_above_fp32_mfma(pkg, dev):
+    """The split-bf16 matrix form is not a reduced precision: on the north-star
+    fixture (reference CPU fp32 loss / Y / gradient), its deviation from the
+    reference is within 1.25x (+ a 1e-7-relative floor) of the fp32-input MFMA
+    form's, for Y and every gradient element; and the default build does use it
+    for both the phase and the weight-gradient kernels (matrix_form == 3)."""
+    g = _load(os.path.join(GOLDEN, "g2_north_star.npz"))
+    layers = [int(v) for v in g["layers"]]
+    D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
+    m = pkg.BlackScholesBarenblatt(g["Xi"], float(g["T"]), M, N, D, layers, "NAIS-Net", "Sine", device=dev)
+    np.random.seed(int(g["batch_seed"]))
+    t, W = m.fetch_minibatch()
+    err = {}
+    for x3 in (True, False):
+        s = make_solver(pkg, dev, g, x3=x3)
+        assert s.matrix_form == (3 if x3 else 0)
+        params = torch.from_numpy(g["params"]).to(dev)
+        grad, loss = torch.empty_like(params), torch.empty(1, device=dev)
+        Y = torch.empty(M * (N + 1), device=dev)
+        s.loss_grad(params, M, N, torch.from_numpy(g["Xi"]).to(dev), t=t.reshape(M, N + 1).float().contiguous(),
+                    W=W.float().contiguous(), grad=grad, loss=loss, Y=Y)
+        torch.cuda.synchronize()
+        used = g["used"]
+        err[x3] = (np.abs(Y.cpu().numpy() - g["Y"].reshape(-1)).max(),
+                   np.abs(grad.cpu().numpy()[used] - g["grad"][used]).max(),
+                   abs(float(loss) - float(g["loss"])))
+    (ey3, eg3, el3), (ey, eg, el) = err[True], err[False]
+    assert ey3 <= 1.25 * ey + 1e-7 * np.abs(g["Y"]).max(), err
+    assert eg3 <= 1.25 * eg + 1e-7 * np.abs(g["grad"]).max(), err
+    assert el3 <= 1.25 * el + 1e-7 * abs(float(g["loss"])), err
