@@ -751,7 +751,7 @@ ChainArgs base_args(dbsde_ctx* c) {
   return a;
 }
 
-constexpr int ROW_PAD = 64;   // rows per phase-kernel workgroup (P3_ROWS) and chain-GEMM tile
+constexpr int ROW_PAD = P3_ROWS;   // rows per phase-kernel workgroup (a multiple of the chain-GEMM tile, 64)
 
 RolloutArgs rollout_args(dbsde_ctx* c, const dbsde_batch* b) {
   const dbsde_problem& pr = c->cfg.problem;
@@ -1435,17 +1435,18 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     const double byA = 4.0 * R * (c->Dp + 4.0 * S + 8.0);
     const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
     const double byC = 4.0 * R * (4.0 * c->Dp + 5.0 * S);
-    // chunks of whole paths and whole 64-row tiles (64 paths = 64 (N+1) rows)
+    // chunks of whole paths and whole P3_ROWS-row tiles (P3_ROWS paths =
+    // P3_ROWS (N+1) rows = N+1 tiles)
     int nch = grad ? c->chunks : 1;
-    while (nch > 1 && (M % 64 != 0 || (M / 64) % nch != 0)) --nch;
+    while (nch > 1 && (M % P3_ROWS != 0 || (M / P3_ROWS) % nch != 0)) --nch;
     if (nch <= 1) {
       RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, c->phase_pad, s>>>(fa));
     } else {
       // phase A / phase C of chunk i on stream (i even ? main : pipe2); the
       // two phases are timed as one pipelined segment
-      // chunk sizes in units of 64 paths; DBSDE_CHUNK0 sets the first chunk's
+      // chunk sizes in units of P3_ROWS paths; DBSDE_CHUNK0 sets the first chunk's
       // units (the rest split evenly), else all chunks are equal
-      const int units = M / 64, utile = N1;   // 64 paths = N1 tiles of 64 rows
+      const int units = M / P3_ROWS, utile = N1;   // P3_ROWS paths = N1 tiles
       std::vector<int> cu(nch, units / nch);
       if (c->chunk0 > 0 && c->chunk0 < units && nch == 2) {
         cu[0] = c->chunk0;

@@ -2,7 +2,8 @@
 //
 // The two network passes of one deep-BSDE step, one wavefront per 16 rows
 // (= 16 (path, time) pairs), 4 waves (64 rows, one wave per SIMD) per
-// workgroup, two workgroups per CU:
+// workgroup, two workgroups per CU (8-wave / 128-row workgroups sharing each
+// staged weight piece measured slower: 0.305 -> 0.366 ms for the phases):
 //   phaseA : forward (a_j, h_j, u) + input gradient (delta_j, g_j, Z) + the
 //            per-row sums the residual needs (net_u, DeepBSDE.py:189-194)
 //   phaseC : residuals and closed-form cotangents (ubar, zbar) of its rows,
@@ -413,7 +414,7 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, SG& sg,
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, {[Z_j], B_j} j=K..1, Z0
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT, bool HV, bool X3>
-__global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
+__global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseA_kernel(FusedArgs p) {
   constexpr bool PFA = true;    // group-ahead fragment prefetch (sgemm_piece)
   constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[(X3 ? 3 : 2) * BUF];
@@ -577,7 +578,7 @@ __global__ void __launch_bounds__(256, 2) phaseA_kernel(FusedArgs p) {
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, B_j j=K..1
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT, bool HV, bool X3>
-__global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
+__global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseC_kernel(FusedArgs p) {
 #ifndef DBSDE_PFC_T
 #define DBSDE_PFC_T true
 #endif
@@ -646,7 +647,16 @@ __global__ void __launch_bounds__(256, 2) phaseC_kernel(FusedArgs p) {
   zero(ad[0]);
   stage_mm<X3, T, TD, TD, T, PFC_T>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
     fload(av, p.Abuf, S, row0, 0);
-    if (threadIdx.x == 0) p.loss_part[tile] = (lsum[0] + lsum[1]) + (lsum[2] + lsum[3]);
+    if (threadIdx.x == 0) {   // fixed-order pairwise tree over the waves
+      double l[P3_WAVES];
+#pragma unroll
+      for (int w = 0; w < P3_WAVES; ++w) l[w] = lsum[w];
+#pragma unroll
+      for (int h = 1; h < P3_WAVES; h <<= 1)
+#pragma unroll
+        for (int w = 0; w + h < P3_WAVES; w += 2 * h) l[w] += l[w + h];
+      p.loss_part[tile] = l[0];
+    }
   });
 #pragma unroll
   for (int o = 0; o < T; ++o)

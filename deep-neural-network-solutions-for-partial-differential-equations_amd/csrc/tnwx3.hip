@@ -13,8 +13,9 @@
 // of B, eight dword loads per block.  One wave per SIMD (a 1024-wave grid):
 // the 7x7 accumulator tile sits in AGPRs (this unit is built with the default
 // MFMA register form), the split B operands of the step (84 VGPRs), the raw
-// next step (112) and one split A block in VGPRs; the next step's loads are
-// issued a whole step (294 MFMAs) ahead.
+// next step (112) and two split A blocks in VGPRs; the next step's loads are
+// issued a whole step (294 MFMAs) ahead, and every A split runs between the
+// MFMAs of the previous block (x3_product).
 #include "tnw.hpp"
 
 namespace dbsde {
@@ -59,30 +60,38 @@ __device__ __forceinline__ void load_cols(float (&r)[NB][8], const float* X, int
   }
 }
 
-// acc += A[rows]^T B[rows] over 32-row steps [g0, g1)
+// acc += A[rows]^T B[rows] over 32-row steps [g0, g1).  Per step: the B
+// split (VALU) and the next step's B loads, then one scheduling region per
+// A block m: its 42 MFMAs with the split of A block m + 1 interleaved one
+// VALU per MFMA gap, and the next step's loads of A block m + 1.  The regions
+// are pinned (sched_barrier): left alone, the scheduler sinks the next step's
+// loads to the top of the next trip, right before their use.
 template <int NB>
 __device__ __forceinline__ void x3_product(floatx4 (&acc)[NB][NB], const float* A, int lda, const float* B, int ldb,
                                            int g0, int g1, int i, int q) {
   float ra[NB][8], rb[NB][8];
-  load_cols<NB>(ra, A, lda, 32 * g0 + 8 * q, i);
   load_cols<NB>(rb, B, ldb, 32 * g0 + 8 * q, i);
+  load_cols<NB>(ra, A, lda, 32 * g0 + 8 * q, i);
+  Split3 sa = split8(ra[0]);   // A block 0 of the step (the last region splits the next step's)
   for (int g = g0; g < g1; ++g) {
     const int nrow = 32 * min(g + 1, g1 - 1) + 8 * q;   // clamped prefetch, unused past the slice
-    // pinned regions (sched_barrier): left alone, the scheduler sinks the
-    // next step's loads to the top of the next trip, right before their use
     Split3 sb[NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) sb[n] = split8(rb[n]);
     __builtin_amdgcn_sched_barrier(0);
     load_cols<NB>(rb, B, ldb, nrow, i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ra[0][j] = A[(size_t)(nrow + j) * lda + i];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int m = 0; m < NB; ++m) {
-      const Split3 sa = split8(ra[m]);
-      __builtin_amdgcn_sched_barrier(0);
+      // region m splits A block m + 1 of this step, the last region block 0 of
+      // the next step (loaded at this step's top)
+      const Split3 san = split8(ra[m + 1 < NB ? m + 1 : 0]);
+      if (m + 1 < NB) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ra[m][j] = A[(size_t)(nrow + j) * lda + 16 * m + i];
-      __builtin_amdgcn_sched_barrier(0);
+        for (int j = 0; j < 8; ++j) ra[m + 1][j] = A[(size_t)(nrow + j) * lda + 16 * (m + 1) + i];
+      }
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         floatx4 c = acc[m][n];
@@ -93,7 +102,14 @@ __device__ __forceinline__ void x3_product(floatx4 (&acc)[NB][NB], const float* 
         c = mfma_bf(sa.h, sb[n].m, c);
         acc[m][n] = mfma_bf(sa.h, sb[n].h, c);
       }
+#pragma unroll
+      for (int k = 0; k < 6 * NB; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // VALU
+      }
+      if (m + 1 < NB) __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);   // VMEM read
       __builtin_amdgcn_sched_barrier(0);
+      sa = san;
     }
   }
 }

@@ -98,6 +98,14 @@ def build(name):
     csrc = os.path.join(tmp, "pkg", "csrc")          # csrc/../../include resolves to tmp/include
     shutil.copytree(os.path.join(PKG, "csrc"), csrc)
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+    if name == "tnwhit":   # weight-gradient x3 operand loads from a fixed 32-row block (cache hits)
+        tx = os.path.join(csrc, "tnwx3.hip")
+        t = open(tx).read()
+        t2 = t.replace("const float* p = X + (size_t)(row0 + j) * ld + i;", "const float* p = X + (size_t)(j + 8 * (row0 & 31) / 8) * ld + i;")
+        t2 = t2.replace("ra[m + 1][j] = A[(size_t)(nrow + j) * lda", "ra[m + 1][j] = A[(size_t)(j + (nrow & 31)) * lda")
+        t2 = t2.replace("ra[0][j] = A[(size_t)(nrow + j) * lda", "ra[0][j] = A[(size_t)(j + (nrow & 31)) * lda")
+        assert t2.count("nrow & 31") == 2, "tnwhit edit"
+        open(tx, "w").write(t2)
     ph = os.path.join(csrc, "phase.hpp")
     s = open(ph).read()
     defs = []
@@ -109,6 +117,8 @@ def build(name):
         defs = ["-DDBSDE_PRIO_EPI"]
     elif name == "priomfma":  # the opposite
         defs = ["-DDBSDE_PRIO_MFMA"]
+    elif name == "tnwhit":
+        pass
     elif name == "pfcr":    # prefetch also in phase C's reverse stages (spills 4 VGPRs)
         defs = ["-DDBSDE_PFC_R=true"]
     else:
