@@ -75,7 +75,6 @@ struct dbsde_ctx {
   // cross-stream event hops cost more than the overlap of the small prep /
   // loss kernels gains, -12 us/step measured); DBSDE_SERIAL=0 forks them.
   int serial = 3;
-  int phase_pad = 0;   // extra dynamic LDS per phase workgroup (occupancy experiments, DBSDE_PHASE_PAD bytes)
   hipEvent_t ev_pipe[2] = {nullptr, nullptr};
   hipEvent_t ev_more[2] = {nullptr, nullptr};
   hipEvent_t ev_prof[2] = {nullptr, nullptr};
@@ -1344,7 +1343,6 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     if (const char* ch = getenv("DBSDE_CHUNK0")) c->chunk0 = atoi(ch);
     if (const char* ch = getenv("DBSDE_PIPES")) c->pipes = std::max(2, std::min(4, atoi(ch)));
     if (const char* ch = getenv("DBSDE_SERIAL")) c->serial = atoi(ch);
-    if (const char* ch = getenv("DBSDE_PHASE_PAD")) c->phase_pad = std::max(0, std::min(100000, atoi(ch)));
     if (e != hipSuccess) rc = fail(c, DBSDE_EHIP, std::string("side stream: ") + hipGetErrorString(e));
   }
   if (rc) {
@@ -1440,7 +1438,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     int nch = grad ? c->chunks : 1;
     while (nch > 1 && (M % P3_ROWS != 0 || (M / P3_ROWS) % nch != 0)) --nch;
     if (nch <= 1) {
-      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, c->phase_pad, s>>>(fa));
+      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
     } else {
       // phase A / phase C of chunk i on stream (i even ? main : pipe2); the
       // two phases are timed as one pipelined segment
@@ -1488,7 +1486,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     }
     if (grad) {
       if (nch <= 1)
-        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / P3_ROWS, 64 * P3_WAVES, c->phase_pad, s>>>(fa));
+        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
       nloss_parts = Rp / P3_ROWS;
     } else {
       RUN(c, "loss_rows", 0.0, 4.0 * R * 3.0 * D,

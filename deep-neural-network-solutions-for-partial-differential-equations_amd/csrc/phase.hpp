@@ -196,11 +196,6 @@ struct PieceStagerT {
   }
   template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
-#if defined(DBSDE_PRIO_EPI)
-    __builtin_amdgcn_s_setprio(0);   // experiment: epilogues at priority 1, MFMA segments at 0
-#elif defined(DBSDE_PRIO_MFMA)
-    __builtin_amdgcn_s_setprio(1);
-#endif
 #ifdef DBSDE_STAMPS
     ts[3 * st] = __builtin_amdgcn_s_memtime();
 #endif
@@ -341,13 +336,15 @@ __device__ __forceinline__ void sgemm_x3_piece(Mat<TO>& acc, const Split3& s, co
       for (int p = 0; p < 3; ++p) w[0][p] = im[(3 * o + p) * 64 + lane];
     }
     if constexpr (NEXT && o < 4) split_pair<TI, NEXT ? KBN : 0, o>(b, sn[0], sn[1], sn[2]);
+    // in the order the fragment parts arrive (hi, mid, lo: counted lgkmcnt
+    // waits let the first MFMAs start before the later reads land)
     const uintx4* wc = w[PF ? (o & 1) : 0];
     floatx4 a = acc.v[o];
-    a = mfma_bf(wc[2], s.h, a);
     a = mfma_bf(wc[0], s.l, a);
+    a = mfma_bf(wc[0], s.m, a);
     a = mfma_bf(wc[1], s.m, a);
     a = mfma_bf(wc[1], s.h, a);
-    a = mfma_bf(wc[0], s.m, a);
+    a = mfma_bf(wc[2], s.h, a);
     acc.v[o] = mfma_bf(wc[0], s.h, a);
     if constexpr (!PF || o + 1 < TO) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // DS read
 #pragma unroll
@@ -402,11 +399,6 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, SG& sg,
     sgemm_piece<TO, TI, H, TI, PF>(acc, b, w, lane);
     sg.mark();
   }
-#if defined(DBSDE_PRIO_EPI)
-  __builtin_amdgcn_s_setprio(1);
-#elif defined(DBSDE_PRIO_MFMA)
-  __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -579,15 +571,9 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseA_kernel(FusedArgs p) {
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT, bool HV, bool X3>
 __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseC_kernel(FusedArgs p) {
-#ifndef DBSDE_PFC_T
-#define DBSDE_PFC_T true
-#endif
-#ifndef DBSDE_PFC_R
-#define DBSDE_PFC_R false
-#endif
   // prefetch in the tangent / reverse stages (the split-bf16 form is at the
   // register limit without it)
-  constexpr bool PFC_T = X3 ? false : DBSDE_PFC_T, PFC_R = X3 ? false : DBSDE_PFC_R;
+  constexpr bool PFC_T = !X3, PFC_R = false;
   constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[(X3 ? 3 : 2) * BUF];
   __shared__ double lsum[P3_WAVES];

@@ -14,7 +14,8 @@ variants break the numerics on purpose -- timing only.
             (H, Delta, Hdot, Alpha, zbar); Abuf/G/zfull (read by phase C) cached
   ntsel2    the complement of ntsel
   noslp     -fno-slp-vectorize (no v_pk_* f32 packing)
-  pfcr      group-ahead fragment prefetch in phase C's reverse stages too
+  tnwhit    weight-gradient x3 kernel loading one fixed 32-row block (cache hits)
+  nostoreall / noloadall / bareall  every activation store / load / both, + nostage
   stamps    -DDBSDE_STAMPS: per-piece s_memtime (wait / MFMA issue / post)
             printed for three tiles -- diagnostic only
   quadplain quad-order stores of the weight-gradient operands without the
@@ -113,14 +114,8 @@ def build(name):
         defs = ["-DDBSDE_STAMPS"]
     elif name == "noslp":   # no SLP packing of f32 elementwise work into v_pk_* (MI355X_MICROARCH: anti-lever beside MFMA)
         defs = ["-fno-slp-vectorize"]
-    elif name == "prioepi":   # s_setprio 1 in epilogues, 0 in MFMA segments
-        defs = ["-DDBSDE_PRIO_EPI"]
-    elif name == "priomfma":  # the opposite
-        defs = ["-DDBSDE_PRIO_MFMA"]
     elif name == "tnwhit":
         pass
-    elif name == "pfcr":    # prefetch also in phase C's reverse stages (spills 4 VGPRs)
-        defs = ["-DDBSDE_PFC_R=true"]
     else:
         s2 = edit(s, name)
         assert s2 != s, name
