@@ -173,6 +173,7 @@ def main():
     ap.add_argument("--workload", default="bsb", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-iters", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prefetch", action="store_true", help="A/B: roll each step's paths out in the step itself")
     ap.add_argument("--activation", default=None, help="experiments only; the headline is Sine")
     ap.add_argument("--mode", default=None, help="experiments only; the headline is NAIS-Net")
     args = ap.parse_args()
@@ -200,13 +201,14 @@ def main():
         torch.cuda.synchronize(dev)
 
     it = 0
+    # each step prefetches the next step's device rollout (device_step next_seed)
     for _ in range(args.warmup):
-        model.device_step(opt, LR, seed=it)
+        model.device_step(opt, LR, seed=it, next_seed=None if args.no_prefetch else it + 1)
         it += 1
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = model.device_step(opt, LR, seed=it)
+        loss = model.device_step(opt, LR, seed=it, next_seed=None if args.no_prefetch else it + 1)
         it += 1
     barrier()
     elapsed = time.perf_counter() - t0
@@ -234,7 +236,7 @@ def main():
     model.solver.profile(True)
     model.solver.profile_reset()
     for _ in range(args.steps):
-        model.device_step(opt, LR, seed=it)
+        model.device_step(opt, LR, seed=it, next_seed=None if args.no_prefetch else it + 1)
         it += 1
     prof = model.solver.profile_read()
     model.solver.profile(False)

@@ -25,7 +25,7 @@ ABI_VERSION = 2
 # every symbol include/dbsde.h declares (checked by the CPU test suite)
 EXPORTED = [
     "dbsde_abi_version", "dbsde_create", "dbsde_destroy", "dbsde_last_error", "dbsde_set_stream",
-    "dbsde_param_count", "dbsde_param_used_mask", "dbsde_matrix_form", "dbsde_brownian_dim", "dbsde_set_corr", "dbsde_brownian",
+    "dbsde_param_count", "dbsde_param_used_mask", "dbsde_matrix_form", "dbsde_brownian_dim", "dbsde_set_corr", "dbsde_brownian", "dbsde_prefetch",
     "dbsde_loss_grad", "dbsde_net_u", "dbsde_optimizer_step", "dbsde_exact", "dbsde_hjb_mc",
     "dbsde_profile_enable", "dbsde_profile_count", "dbsde_profile_read", "dbsde_profile_reset",
 ]
@@ -91,6 +91,7 @@ def load():
         "dbsde_brownian_dim": (i, [vp]),
         "dbsde_set_corr": (i, [vp, vp, i]),
         "dbsde_brownian": (i, [vp, ctypes.POINTER(Batch), vp, vp, i]),
+        "dbsde_prefetch": (i, [vp, ctypes.POINTER(Batch)]),
         "dbsde_exact": (i, [i, vp, vp, ll, i, ctypes.c_float, vp, vp, vp, vp]),
         "dbsde_hjb_mc": (i, [vp, vp, i, i, ctypes.c_float, ll, ctypes.c_ulonglong, vp, vp]),
         "dbsde_loss_grad": (i, [vp, vp, ctypes.POINTER(Batch), vp, ctypes.POINTER(Outputs)]),

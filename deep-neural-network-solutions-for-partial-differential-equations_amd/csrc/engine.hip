@@ -66,6 +66,17 @@ struct dbsde_ctx {
   // (weight repack during the rollout, loss sum and grad clear during phase C)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
+  // path buffers (xin, sdw) x 2: a device-mode rollout can be prefetched into
+  // the buffer the queued work no longer reads (dbsde_prefetch) on pf_stream
+  float* xin_b[2] = {nullptr, nullptr};
+  float* sdw_b[2] = {nullptr, nullptr};
+  struct Pending {
+    bool valid = false;
+    dbsde_batch b{};
+    hipEvent_t ready = nullptr;
+  } pend[2];
+  hipStream_t pf_stream = nullptr;
+  hipEvent_t ev_pf_order = nullptr;
   // path-chunked phase pipeline: chunk i runs phase A then phase C on stream
   // pipe[i % 2], so one chunk's phase C fills the other's phase-A tail
   hipStream_t pipe2 = nullptr;
@@ -671,6 +682,8 @@ int ensure_rows(dbsde_ctx* c, int Rp, int N) {
   const int nr = std::max(Rp, c->cap_rows), nn = std::max(N, c->cap_n);
   if (!c->row_allocs.empty()) {
     HIPC(c, hipStreamSynchronize(c->stream));
+    if (c->pf_stream) HIPC(c, hipStreamSynchronize(c->pf_stream));
+    c->pend[0].valid = c->pend[1].valid = false;
     for (void* p : c->row_allocs) {
       (void)hipFree(p);
       c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), p));
@@ -681,8 +694,12 @@ int ensure_rows(dbsde_ctx* c, int Rp, int N) {
   const size_t R = nr;
   int rc;
   const int ldx = c->Dp, S = c->Stot;
-  if ((rc = dalloc_t(c, &c->xin, R * ldx))) return rc;
-  if ((rc = dalloc_t(c, &c->sdw, R * ldx))) return rc;
+  for (int i = 0; i < 2; ++i) {
+    if ((rc = dalloc_t(c, &c->xin_b[i], R * ldx))) return rc;
+    if ((rc = dalloc_t(c, &c->sdw_b[i], R * ldx))) return rc;
+  }
+  c->xin = c->xin_b[0];
+  c->sdw = c->sdw_b[0];
   if ((rc = dalloc_t(c, &c->zbar, R * ldx))) return rc;
   if ((rc = dalloc_t(c, &c->zfull, R * ldx))) return rc;
   if ((rc = dalloc_t(c, &c->Abuf, R * S))) return rc;
@@ -800,6 +817,37 @@ int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
     const int nthr = ra.M * ra.D;
     RUN(c, name, 0.0, bytes, rollout_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
   }
+  return DBSDE_OK;
+}
+
+bool same_batch(const dbsde_batch& a, const dbsde_batch& b) {
+  return a.M == b.M && a.N == b.N && a.t == b.t && a.W == b.W && a.seed == b.seed && a.offset == b.offset &&
+         a.path0 == b.path0 && a.Xi == b.Xi && a.xi_rows == b.xi_rows;
+}
+// Point c->xin / c->sdw at the path buffer this call uses.  A device-mode
+// batch that dbsde_prefetch already rolled out takes that buffer (the main
+// stream waits for the prefetch; from_pf = true); anything else takes a
+// buffer no pending prefetch writes.
+int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
+  from_pf = false;
+  int use = -1;
+  if (b && !b->W)
+    for (int i = 0; i < 2 && use < 0; ++i)
+      if (c->pend[i].valid && same_batch(c->pend[i].b, *b)) {
+        use = i;
+        from_pf = true;
+      }
+  if (use < 0) {
+    use = c->pend[0].valid ? (c->pend[1].valid ? 0 : 1) : 0;
+    // both pending and neither is this batch: the older one's buffer is reused
+    // once its rollout is done
+    if (c->pend[use].valid) HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
+  } else {
+    HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
+  }
+  c->pend[use].valid = false;
+  c->xin = c->xin_b[use];
+  c->sdw = c->sdw_b[use];
   return DBSDE_OK;
 }
 
@@ -1339,6 +1387,9 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
       if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventCreate(&c->ev_prof[i]);
     }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pf_order, hipEventDisableTiming);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pend[i].ready, hipEventDisableTiming);
     if (const char* ch = getenv("DBSDE_CHUNKS")) c->chunks = std::max(1, std::min(16, atoi(ch)));
     if (const char* ch = getenv("DBSDE_CHUNK0")) c->chunk0 = atoi(ch);
     if (const char* ch = getenv("DBSDE_PIPES")) c->pipes = std::max(2, std::min(4, atoi(ch)));
@@ -1360,7 +1411,13 @@ void dbsde_destroy(dbsde_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->pipe2) (void)hipStreamSynchronize(c->pipe2);
+  if (c->pf_stream) {
+    (void)hipStreamSynchronize(c->pf_stream);
+    (void)hipStreamDestroy(c->pf_stream);
+  }
+  if (c->ev_pf_order) (void)hipEventDestroy(c->ev_pf_order);
   for (int i = 0; i < 2; ++i) {
+    if (c->pend[i].ready) (void)hipEventDestroy(c->pend[i].ready);
     if (c->ev_fork[i]) (void)hipEventDestroy(c->ev_fork[i]);
     if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
     if (c->ev_pipe[i]) (void)hipEventDestroy(c->ev_pipe[i]);
@@ -1412,9 +1469,12 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   // weight repack (projection, norms, fragment images) overlaps the rollout
   if ((rc = fork_side(c, 0, [&]() { return prep_weights(c, params); }))) return rc;
 
-  // ---- rollout (network-independent: mu/sigma never read Y, Z)
-  if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
-  {
+  // ---- rollout (network-independent: mu/sigma never read Y, Z), unless
+  // dbsde_prefetch already produced this batch's paths
+  bool from_pf = false;
+  if ((rc = select_paths(c, b, from_pf))) return rc;
+  if (!from_pf) {
+    if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
     RolloutArgs ra = rollout_args(c, b);
     ra.out = PATH_ROLLOUT;
     if ((rc = launch_paths(c, ra))) return rc;
@@ -1725,6 +1785,8 @@ int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const 
   hipStream_t s = c->stream;
   if ((rc = prep_weights(c, params))) return rc;
   const long long n = (long long)Rp * c->Dp;
+  bool from_pf;
+  if ((rc = select_paths(c, nullptr, from_pf))) return rc;
   RUN(c, "netu_input", 0.0, 0.0,
       netu_input_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
   if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
@@ -1793,6 +1855,9 @@ int dbsde_brownian_dim(const dbsde_ctx* c) { return c ? c->nb : -1; }
 int dbsde_set_corr(dbsde_ctx* c, const float* L, int n) {
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
   HIPC(c, hipSetDevice(c->device));
+  // a prefetched rollout read the old factor: drop it (and let it finish)
+  if (c->pf_stream) HIPC(c, hipStreamSynchronize(c->pf_stream));
+  c->pend[0].valid = c->pend[1].valid = false;
   if (!L) {
     if (c->Lt) {
       HIPC(c, hipStreamSynchronize(c->stream));
@@ -1812,6 +1877,46 @@ int dbsde_set_corr(dbsde_ctx* c, const float* L, int n) {
   if (!c->Lt && (rc = dalloc_t(c, &c->Lt, (size_t)n * n))) return rc;
   HIPC(c, hipStreamSynchronize(c->stream));
   HIPC(c, hipMemcpy(c->Lt, lt.data(), lt.size() * sizeof(float), hipMemcpyHostToDevice));
+  return DBSDE_OK;
+}
+
+int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  int rc = validate_batch(c, next);
+  if (rc) return rc;
+  if (next->W || next->t) return fail(c, DBSDE_EINVAL, "dbsde_prefetch: device-mode batches only (t and W NULL)");
+  HIPC(c, hipSetDevice(c->device));
+  const int M = next->M, N = next->N, R = M * (N + 1), Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD;
+  if ((rc = ensure_rows(c, Rp, N))) return rc;
+  for (int i = 0; i < 2; ++i)
+    if (c->pend[i].valid && same_batch(c->pend[i].b, *next)) return DBSDE_OK;   // already queued
+  // a buffer no pending prefetch holds (else the first one's is replaced: its
+  // rollout is earlier on the same stream)
+  const int j = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : 0);
+  // after everything queued so far on the caller's stream (Xi ready, the
+  // buffer's previous readers done); work queued later overlaps this
+  HIPC(c, hipEventRecord(c->ev_pf_order, c->stream));
+  HIPC(c, hipStreamWaitEvent(c->pf_stream, c->ev_pf_order, 0));
+  hipStream_t main_stream = c->stream;
+  float *xin0 = c->xin, *sdw0 = c->sdw;
+  c->stream = c->pf_stream;
+  c->xin = c->xin_b[j];
+  c->sdw = c->sdw_b[j];
+  hipError_t e = hipSuccess;
+  if (Rp > R) e = hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, c->stream);
+  if (e == hipSuccess) {
+    RolloutArgs ra = rollout_args(c, next);
+    ra.out = PATH_ROLLOUT;
+    rc = launch_paths(c, ra);
+  }
+  c->stream = main_stream;
+  c->xin = xin0;
+  c->sdw = sdw0;
+  if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("prefetch: ") + hipGetErrorString(e));
+  if (rc) return rc;
+  HIPC(c, hipEventRecord(c->pend[j].ready, c->pf_stream));
+  c->pend[j].valid = true;
+  c->pend[j].b = *next;
   return DBSDE_OK;
 }
 

@@ -311,15 +311,24 @@ class FBSNN(ABC):
         self._update(opt_state, learning_rate, skip_loss=loss if self.skip_nonfinite else None)
         return loss, out
 
-    def device_step(self, opt_state, learning_rate=None, seed=0, optimizer_type=None):
+    def device_step(self, opt_state, learning_rate=None, seed=0, optimizer_type=None, next_seed=None):
         """Throughput-mode iteration: Brownian increments drawn on the device
         (Philox keyed by global path index, correlated by L when set),
         loss+grad, all-reduce, clip + optimizer.  No host synchronisation;
-        returns the device loss."""
+        returns the device loss.  next_seed: the seed of the following
+        iteration, whose rollout is then prefetched to overlap this one
+        (dbsde_prefetch); the numbers are the same either way."""
         if self._L is not None and self.spec.kind != "diag":
             raise NotImplementedError("device-mode correlated increments are implemented for diagonal problems")
         p0, ml = self._local_slice(self.M)
-        self.solver.loss_grad(self.params, ml, self.N, self._local_xi(p0, ml, self.M), seed=seed, path0=p0,
+        key = (p0, ml, self.M, self.N, id(self.Xi))
+        if getattr(self, "_xi_dev_key", None) != key:   # one Xi tensor per shard (the prefetch matches its pointer)
+            self._xi_dev = self._local_xi(p0, ml, self.M).clone()
+            self._xi_dev_key = key
+        xi = self._xi_dev
+        if next_seed is not None:
+            self.solver.prefetch(ml, self.N, xi, seed=next_seed, path0=p0)
+        self.solver.loss_grad(self.params, ml, self.N, xi, seed=seed, path0=p0,
                               grad=self.grad, loss=self._gradbuf[-1:])
         loss = self._reduce()
         self._update(opt_state, learning_rate, skip_loss=loss if self.skip_nonfinite else None)
@@ -333,7 +342,8 @@ class FBSNN(ABC):
         losses = []
         for it in range(previous_it, previous_it + N_Iter):
             self._schedule_n(it)
-            losses.append(self.device_step(opt_state, learning_rate, seed=(seed << 20) + it).clone())
+            nxt = (seed << 20) + it + 1 if it + 1 < previous_it + N_Iter else None
+            losses.append(self.device_step(opt_state, learning_rate, seed=(seed << 20) + it, next_seed=nxt).clone())
             if it % self.log_every == 0:
                 self.training_loss.append(float(torch.cat(losses).mean()))
                 losses = []

@@ -139,6 +139,20 @@ class NativeSolver:
         _lib.check(self.lib.dbsde_loss_grad(self.ctx, _ptr(params), ctypes.byref(b), _ptr(grad),
                                             ctypes.byref(o)), self.ctx)
 
+    def prefetch(self, M, N, Xi, seed=0, offset=0, path0=0):
+        """Roll out the device-mode batch a later loss_grad(M, N, Xi, seed=...,
+        offset=..., path0=...) with the same Xi tensor will consume, on an
+        internal stream overlapping the work queued after this call
+        (dbsde_prefetch).  Xi must stay unchanged (and alive) until then."""
+        D = self.D
+        self._check_tensor(Xi, "Xi")
+        if Xi.numel() not in (D, M * D):
+            raise ValueError("Xi must hold 1 or M rows of D values")
+        b = _lib.Batch(int(M), int(N), None, None, int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1),
+                       int(path0), _ptr(Xi), Xi.numel() // D)
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_prefetch(self.ctx, ctypes.byref(b)), self.ctx)
+
     def net_u(self, params, t, X, u, Du):
         R = X.numel() // self.D
         self._check_tensor(params, "params", self.nparams)

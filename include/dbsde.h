@@ -182,6 +182,21 @@ typedef struct dbsde_outputs {
 int dbsde_brownian(dbsde_ctx* ctx, const dbsde_batch* batch, float* t, float* W, int increments);
 
 /*
+ * Roll out a device-mode batch ahead of the dbsde_loss_grad that consumes it
+ * (the reference's next fetch_minibatch, DeepBSDE.py:247-262, drawn while the
+ * current iteration runs: train() draws each iteration's batch independently
+ * of the model, nd_BSPDE_case.py:371).  The rollout runs on an internal
+ * stream ordered after the work already queued on the context's stream, so
+ * work queued later (the current iteration) overlaps it.  A later
+ * dbsde_loss_grad whose batch descriptor is identical (M, N, seed, offset,
+ * path0, Xi pointer and rows; t = W = NULL) uses the prefetched paths instead
+ * of rolling out; any other batch rolls out as usual.  At most two batches
+ * are pending.  Xi is read when the prefetch runs: it must not change after
+ * this call.  dbsde_set_corr drops pending prefetches.
+ */
+int dbsde_prefetch(dbsde_ctx* ctx, const dbsde_batch* next);
+
+/*
  * FBSNN.loss_function + loss.backward (DeepBSDE.py:202-245, 279).
  * grad (device, flat, param_count) receives d loss / d params (overwritten,
  * 0 for unused parameters); grad == NULL runs the forward only (predict,

@@ -138,3 +138,40 @@ def test_heston_device_mode(pkg, dev, k):
     X = device_X(pkg, dev, s, M, N, Xi, seed=2)
     Xr, _ = ph.heston_rollout(Xi, dW, T)
     np.testing.assert_array_equal(X, Xr)
+
+
+def test_prefetched_rollout_is_the_same_step(pkg, dev):
+    """dbsde_prefetch (the next iteration's rollout on the library's prefetch
+    stream, overlapping the current one): a loss_grad that consumes a
+    prefetched batch returns bit-identical X, loss and gradient to one that
+    rolls out itself; a mismatching batch (other seed) is rolled out as usual;
+    two batches may be pending at once; a width-110 NAIS-Net (split-bf16
+    kernels) and the Cholesky-correlated path kernel both take this route."""
+    D, M, N = 100, 128, 10
+    rs = np.random.RandomState(3)
+    L = np.linalg.cholesky(np.corrcoef(rs.normal(size=(D, 3 * D))) + 1e-3 * np.eye(D)).astype(np.float32)
+    for corr in (False, True):
+        s = solver(pkg, dev, D, pkg.ProblemSpec(**BASKET), layers=[D + 1] + 4 * [110] + [1])
+        if corr:
+            s.set_corr(L)
+        params = torch.from_numpy(rs.normal(scale=0.05, size=s.nparams).astype(np.float32)).to(dev)
+        Xi = torch.ones(D, device=dev)
+
+        def step(seed):
+            X = torch.empty(M * (N + 1) * D, device=dev)
+            grad, loss = torch.empty_like(params), torch.empty(1, device=dev)
+            s.loss_grad(params, M, N, Xi, seed=seed, grad=grad, loss=loss, X=X)
+            torch.cuda.synchronize()
+            return X.cpu().numpy(), float(loss), grad.cpu().numpy()
+
+        ref = {k: step(k) for k in (5, 6, 7)}
+        s.prefetch(M, N, Xi, seed=5)
+        s.prefetch(M, N, Xi, seed=6)            # two pending
+        got5 = step(5)
+        s.prefetch(M, N, Xi, seed=9)            # replaced below: seed 7 is not the prefetched one
+        got7 = step(7)
+        got6 = step(6)
+        for a, b in ((got5, ref[5]), (got6, ref[6]), (got7, ref[7])):
+            np.testing.assert_array_equal(a[0], b[0])
+            assert a[1] == b[1]
+            np.testing.assert_array_equal(a[2], b[2])
