@@ -1323,12 +1323,15 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
   auto addC = [&](const float* img, int TO, int TI) { add(a.simgC, a.snfC, a.nC, img, TO, TI); };
   addA(c->imgX[0], TW, TDp);
   addC(c->imgX[0], TW, TDp);
+  const bool xfirst = c->x3 && c->has_v;   // phase C's X-first stage order (phase.hpp)
+  if (xfirst)
+    for (int j = 1; j <= K; ++j) addC(c->imgX[j], TW, TDp);
   for (int j = 1; j <= K; ++j) {
     addA(c->imgF[j], TW, TW);
     addC(c->imgF[j], TW, TW);
     if (c->has_v) {
       addA(c->imgX[j], TW, TDp);
-      addC(c->imgX[j], TW, TDp);
+      if (!xfirst) addC(c->imgX[j], TW, TDp);
     }
   }
   for (int j = K; j >= 1; --j) {

@@ -573,7 +573,7 @@ template <int T, int TD, int K, int ACT, bool HV, bool X3>
 __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseC_kernel(FusedArgs p) {
   // prefetch in the tangent / reverse stages (the split-bf16 form is at the
   // register limit without it)
-  constexpr bool PFC_T = !X3, PFC_R = false;
+  constexpr bool PFC_T = !X3 || (HV && ACT != ACT_TANH), PFC_R = false;   // tanh: register-bound
   constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
   __shared__ floatx4 wl[(X3 ? 3 : 2) * BUF];
   __shared__ double lsum[P3_WAVES];
@@ -630,6 +630,11 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseC_kernel(FusedArgs p) {
 
   Mat<T> ad[K + 1];   // adot_j
   Mat<T> hd, av;
+  // X-first (split-bf16 NAIS): the x-stack products zbar V_j^T of every
+  // level come first, so zbar is dead before the block stages and the
+  // tangent has the registers for the fragment prefetch.  Image order (host):
+  // X0, X1..XK, F1..FK, B_K..B1 (else X0, {F_j, X_j}, B_K..B1).
+  constexpr bool XFIRST = X3 && HV;
   zero(ad[0]);
   stage_mm<X3, T, TD, TD, T, PFC_T>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
     fload(av, p.Abuf, S, row0, 0);
@@ -644,18 +649,25 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseC_kernel(FusedArgs p) {
       p.loss_part[tile] = l[0];
     }
   });
+  if constexpr (XFIRST) {
+    SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
+      constexpr int j = decltype(jc)::value;
+      zero(ad[j]);
+      stage_mm<X3, T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
+    });
+  }
 #pragma unroll
   for (int o = 0; o < T; ++o)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) hd.v[o][rr] = act_1<ACT>(av.v[o][rr]) * ad[0].v[o][rr];
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    zero(ad[j]);
+    if constexpr (!XFIRST) zero(ad[j]);
     stage_mm<X3, T, T, 0, 2 * T, PFC_T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
       bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd);
       fload(av, p.Abuf, S, row0, j * Wd);
     });
-    if constexpr (HV) stage_mm<X3, T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
+    if constexpr (HV && !XFIRST) stage_mm<X3, T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o)
 #pragma unroll
