@@ -1102,9 +1102,13 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp) {
   if (c->tnw_nb < 1 || c->tnw_nb > 8) return fail(c, DBSDE_EINVAL, "internal: tnw tile");
   if (c->tnw_x3) {
     if (Rp % 32 != 0) return fail(c, DBSDE_EINVAL, "internal: tnw x3 geometry");
-    RUN(c, "tn_weight_grad", fl, 0.0, (void)tnw_x3_launch(c->tnw_nb, a, s));
+    int lr = 0;
+    RUN(c, "tn_weight_grad", fl, 0.0, lr = tnw_x3_launch(c->tnw_nb, a, s));
+    if (lr) return fail(c, DBSDE_EINVAL, "internal: tnw x3 launch geometry");
   } else {
-    RUN(c, "tn_weight_grad", fl, 0.0, (void)tnw_launch(c->tnw_nb, a, s));
+    int lr = 0;
+    RUN(c, "tn_weight_grad", fl, 0.0, lr = tnw_launch(c->tnw_nb, a, s));
+    if (lr) return fail(c, DBSDE_EINVAL, "internal: tnw launch geometry");
   }
   return DBSDE_OK;
 }
