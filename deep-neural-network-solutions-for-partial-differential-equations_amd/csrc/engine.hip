@@ -921,14 +921,15 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
     if (d.fdst) {
       const int dr = (d.transpose ? cc : r) + d.frow0, dc = (d.transpose ? r : cc) + d.fcol0;
       if (d.fsplit) {
-        // v = hi + mid + lo exactly (8 + 8 + 8 significand bits, truncating splits)
+        // v = hi + mid + lo exactly: hi, mid rounded to nearest even, lo the
+        // remainder (phase.hpp split_two)
         unsigned short* img = (unsigned short*)d.fdst + x3_off(dr, dc, d.ftout);
-        const unsigned u = __float_as_uint(v);
-        const float r1 = v - __uint_as_float(u & 0xffff0000u);
-        const unsigned u1 = __float_as_uint(r1);
-        const float r2 = r1 - __uint_as_float(u1 & 0xffff0000u);
-        img[0] = (unsigned short)(u >> 16);
-        img[512] = (unsigned short)(u1 >> 16);
+        const __bf16 h = (__bf16)v;
+        const float r1 = v - (float)h;
+        const __bf16 m = (__bf16)r1;
+        const float r2 = r1 - (float)m;
+        img[0] = __builtin_bit_cast(unsigned short, h);
+        img[512] = __builtin_bit_cast(unsigned short, m);
         img[1024] = (unsigned short)(__float_as_uint(r2) >> 16);
       } else {
         d.fdst[frag_off(dr, dc, d.ftin, d.ftout)] = v;

@@ -246,46 +246,60 @@ struct NoOp {
 
 // ---------------------------------------------------------------------------
 // Split-bf16 products (X3 kernels).  An fp32 value is the exact sum of three
-// bf16 parts, x = hi + mid + lo (truncating splits: 8 + 8 + 8 significand
-// bits), and W x is accumulated as the six v_mfma_f32_16x16x32_bf16 products
-// Wl.xh + Wh.xl + Wm.xm + Wm.xh + Wh.xm + Wh.xh; the three dropped products
-// are below 2^-24 relative.  Every bf16 product is exact in the fp32
-// accumulator, so the result is as accurate as the fp32-input MFMA chain
-// (tools/ubench/x3_acc.hip on the GPU: mean error / sum|w x| 1.6e-8 against
-// 2.0e-8 for v_mfma_f32_16x16x4_f32, max 2.2e-7 against 2.3e-7) at 16/6 of its
-// rate on the matrix cores, which also leave the vector ALUs to the epilogues.
+// bf16 parts, x = hi + mid + lo (hi and mid rounded to nearest even, lo the
+// remainder: 8 + 8 + 8 significand bits), and W x is accumulated as the six
+// v_mfma_f32_16x16x32_bf16 products Wl.xh + Wh.xl + Wm.xm + Wm.xh + Wh.xm +
+// Wh.xh.  Every bf16 product is exact in the fp32 accumulator and the three
+// dropped ones (Wm.xl, Wl.xm, Wl.xl) sum to at most 2^-24 of |W x| (the
+// fp32 rounding bound of the product itself; unbiased, 3.5e-9 on average,
+// tests/test_host_logic.py), so the result is as accurate as the fp32-input
+// MFMA chain (tools/ubench/x3_acc.hip) at 16/6 of its rate on the matrix
+// cores, which also leave the vector ALUs to the epilogues.
 // Operand order: a 32-wide input block kb is the pair of 16-column register
 // blocks (2 kb, 2 kb + 1) of the B-layout tile; lane (cl, q) element j holds
 // column 32 kb + 16 (j >> 2) + 4 q + (j & 3) -- no data movement between
 // layers, the weight image carries the same permutation (x3_off).
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 
 struct Split3 {
   bf16x8 h, m, l;
 };
-__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
-// [upper half of a | upper half of b << 16]: two truncated bf16 in one dword
+// [upper half of a | upper half of b << 16]: two bf16 in one dword (exact
+// when a and b are bf16 values)
 __device__ __forceinline__ unsigned hi_pair(float a, float b) {
   return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
 }
+// (x0, x1) -> dword d of the hi / mid / lo operands: hi = bf16(x) and mid =
+// bf16(x - hi) rounded to nearest even (v_cvt_pk_bf16_f32), lo = the exact
+// remainder (at most 8 significant bits, so a bf16 value)
+struct Dw3 {
+  unsigned h, m, l;
+};
+__device__ __forceinline__ Dw3 split_two(float x0, float x1) {
+  const bf16x2 h = __builtin_convertvector(floatx2{x0, x1}, bf16x2);
+  const float r0 = x0 - (float)h[0], r1 = x1 - (float)h[1];
+  const bf16x2 m = __builtin_convertvector(floatx2{r0, r1}, bf16x2);
+  return Dw3{__builtin_bit_cast(unsigned, h), __builtin_bit_cast(unsigned, m), hi_pair(r0 - (float)m[0], r1 - (float)m[1])};
+}
 template <int TI, int KB>
 __device__ __forceinline__ Split3 split_block(const Mat<TI>& b) {
-  float x[8], r1[8], r2[8];
+  float x[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int t = 2 * KB + (j >> 2);
     x[j] = t < TI ? b.v[t < TI ? t : 0][j & 3] : 0.f;
-    r1[j] = x[j] - trunc_bf16(x[j]);
-    r2[j] = r1[j] - trunc_bf16(r1[j]);
   }
   uintx4 H, M, L;
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    H[d] = hi_pair(x[2 * d], x[2 * d + 1]);
-    M[d] = hi_pair(r1[2 * d], r1[2 * d + 1]);
-    L[d] = hi_pair(r2[2 * d], r2[2 * d + 1]);
+    const Dw3 r = split_two(x[2 * d], x[2 * d + 1]);
+    H[d] = r.h;
+    M[d] = r.m;
+    L[d] = r.l;
   }
   return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, M), __builtin_bit_cast(bf16x8, L)};
 }
@@ -296,17 +310,16 @@ __device__ __forceinline__ floatx4 mfma_bf(uintx4 a, const bf16x8& b, floatx4 c)
 // hi / mid / lo operands
 template <int TI, int KB, int d>
 __device__ __forceinline__ void split_pair(const Mat<TI>& b, uintx4& H, uintx4& M, uintx4& L) {
-  float x[2], r1[2], r2[2];
+  float x[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
     const int j = 2 * d + e, t = 2 * KB + (j >> 2);
     x[e] = t < TI ? b.v[t < TI ? t : 0][j & 3] : 0.f;
-    r1[e] = x[e] - trunc_bf16(x[e]);
-    r2[e] = r1[e] - trunc_bf16(r1[e]);
   }
-  H[d] = hi_pair(x[0], x[1]);
-  M[d] = hi_pair(r1[0], r1[1]);
-  L[d] = hi_pair(r2[0], r2[1]);
+  const Dw3 r = split_two(x[0], x[1]);
+  H[d] = r.h;
+  M[d] = r.m;
+  L[d] = r.l;
 }
 // acc[o] += W(o, kb) . b(kb) over one piece = the TO fragments of input block
 // kb, fragment o at chunks 3 o .. 3 o + 2 (hi, mid, lo).  Each fragment is one

@@ -2,10 +2,10 @@
 // split-bf16 products.
 //
 // Each operand value is the exact sum of three bf16 parts (hi + mid + lo,
-// truncating splits, see phase.hpp) and every 16x16 output block accumulates
-// the six v_mfma_f32_16x16x32_bf16 products al.bh + ah.bl + am.bm + am.bh +
-// ah.bm + ah.bh over a 32-row k-step; the dropped products are below 2^-24
-// relative, so the sums are as accurate as the fp32-input MFMA chain of
+// see phase.hpp) and every 16x16 output block accumulates the six
+// v_mfma_f32_16x16x32_bf16 products al.bh + ah.bl + am.bm + am.bh + ah.bm +
+// ah.bh over a 32-row k-step; the dropped products stay within 2^-24 of each
+// product, so the sums are as accurate as the fp32-input MFMA chain of
 // tnw.hip (tools/ubench/x3_acc.hip) at 16/6 of its matrix rate.
 //
 // Operand layout of a 32-row step: lane (i, q) holds rows 8q .. 8q + 7 of
@@ -29,20 +29,24 @@ struct Split3 {
   bf16x8 h, m, l;
 };
 
-__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ unsigned hi_pair(float a, float b) {
   return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
 }
+// hi = bf16(x), mid = bf16(x - hi) (round to nearest even), lo = the exact
+// remainder (phase.hpp split_two)
 __device__ __forceinline__ Split3 split8(const float (&x)[8]) {
   uintx4 H, M, L;
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    const float x0 = x[2 * d], x1 = x[2 * d + 1];
-    const float r0 = x0 - trunc_bf16(x0), r1 = x1 - trunc_bf16(x1);
-    const float s0 = r0 - trunc_bf16(r0), s1 = r1 - trunc_bf16(r1);
-    H[d] = hi_pair(x0, x1);
-    M[d] = hi_pair(r0, r1);
-    L[d] = hi_pair(s0, s1);
+    const bf16x2 h = __builtin_convertvector(floatx2{x[2 * d], x[2 * d + 1]}, bf16x2);
+    const float r0 = x[2 * d] - (float)h[0], r1 = x[2 * d + 1] - (float)h[1];
+    const bf16x2 m = __builtin_convertvector(floatx2{r0, r1}, bf16x2);
+    H[d] = __builtin_bit_cast(unsigned, h);
+    M[d] = __builtin_bit_cast(unsigned, m);
+    L[d] = hi_pair(r0 - (float)m[0], r1 - (float)m[1]);
   }
   return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, M), __builtin_bit_cast(bf16x8, L)};
 }

@@ -155,3 +155,70 @@ def test_optimizer_names():
         obj._check_optimizer("LBFGS")
     for name in ("Adam", "SGD", "RMSprop", "AdamW", "Adadelta", "Adagrad", "Adamax", "ASGD"):
         obj._check_optimizer(name)
+
+
+def _rne16(x):
+    """fp32 -> the nearest bf16 value (ties to even), as fp32 (v_cvt_pk_bf16_f32)."""
+    u = x.view(np.uint32).astype(np.uint64)
+    return ((((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32)).view(np.float32)
+
+
+def _split3(x):
+    hi = _rne16(x)
+    r1 = (x - hi).astype(np.float32)
+    mid = _rne16(r1)
+    return hi, mid, (r1 - mid).astype(np.float32)
+
+
+def test_split_bf16_parts_are_exact():
+    """The split-bf16 matrix form (csrc/phase.hpp split_two, the pack kernel):
+    x = hi + mid + lo holds exactly for fp32 x (hi, mid rounded to nearest
+    even, lo the remainder), each part is a bf16 value, and the six kept
+    products reproduce the product w x within 2^-24 |w x| -- the fp32 rounding
+    bound of the product itself -- with no bias."""
+    rs = np.random.RandomState(11)
+    n = 400000
+    x = (rs.standard_normal(n) * np.exp(rs.uniform(-30, 30, n))).astype(np.float32)
+    w = rs.standard_normal(n).astype(np.float32)
+    xh, xm, xl = _split3(x)
+    wh, wm, wl = _split3(w)
+    for p in (xh, xm, xl, wl):   # bf16 values: the low 16 bits are clear
+        assert np.all((p.view(np.uint32) & np.uint32(0xFFFF)) == 0)
+    np.testing.assert_array_equal(xh.astype(np.float64) + xm + xl, x.astype(np.float64))
+    d = np.float64
+    six = d(wl) * xh + d(wh) * xl + d(wm) * xm + d(wm) * xh + d(wh) * xm + d(wh) * xh
+    exact = d(w) * d(x)
+    rel = (six - exact) / np.abs(exact)
+    assert np.abs(rel).max() <= 2.0 ** -24
+    assert abs(rel.mean()) < 1e-10 and np.abs(rel).mean() < 1e-8
+
+
+def test_split_bf16_operand_order_is_the_register_layout():
+    """x3_off (csrc/kernels.hpp): the image's k slot (q, j) of 32-wide block kb
+    is input column 32 kb + 16 (j >> 2) + 4 q + (j & 3) -- exactly the columns
+    lane (cl, q) holds in output register blocks 2 kb (j < 4) and 2 kb + 1
+    (j >= 4) of the previous layer -- and the map is a bijection onto the
+    [hi | mid | lo] fragment slots."""
+    def x3_off(o, i, tout):   # restated from kernels.hpp
+        ii = i & 31
+        q = (ii >> 2) & 3
+        j = ((ii >> 4) << 2) | (ii & 3)
+        f = (i >> 5) * tout + (o >> 4)
+        return f * 1536 + ((o & 15) + 16 * q) * 8 + j
+
+    TO, TI = 7, 7
+    seen = set()
+    for o in range(16 * TO):
+        for i in range(16 * TI):
+            off = x3_off(o, i, TO)
+            f, rem = divmod(off, 1536)
+            lane, j = divmod(rem, 8)
+            assert rem < 512                          # the hi part; mid / lo at +512 / +1024
+            cl, q = lane & 15, lane >> 4
+            kb = f // TO
+            assert cl == o % 16 and f % TO == o // 16
+            # the column lane (cl, q) holds in register block t = 2 kb + (j >> 2), component j & 3
+            t = 2 * kb + (j >> 2)
+            assert i == 16 * t + 4 * q + (j & 3)
+            seen.add(off)
+    assert len(seen) == 16 * TO * 16 * TI
