@@ -852,7 +852,8 @@ int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
 }
 
 int prep_weights(dbsde_ctx* c, const float* params);
-int finalize_grads(dbsde_ctx* c, const float* params, float* grad);
+int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double* loss_part = nullptr, int nloss = 0,
+                   float* loss = nullptr);
 
 }  // namespace
 
@@ -1114,13 +1115,13 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp) {
   return DBSDE_OK;
 }
 
-int finalize_grads(dbsde_ctx* c, const float* params, float* grad) {
+int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double* loss_part, int nloss, float* loss) {
   hipStream_t s = c->stream;
   if (c->tnw) {
     const int T = c->Dp;
     RUN(c, "grad_finalize", 0.0, 0.0,
         tilefin_kernel<<<dim3((T * T + TF_ELEMS - 1) / TF_ELEMS, c->tnw_P + 1), 256, 0, s>>>(
-            c->d_fin, c->n_fin, c->slabW, c->tnw_S, c->tnw_P, T, grad));
+            c->d_fin, c->n_fin, c->slabW, c->tnw_S, c->tnw_P, T, grad, loss_part, nloss, loss));
   } else {
     RUN(c, "grad_finalize", 0.0, 0.0, slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad));
   }
@@ -1597,8 +1598,10 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     nloss_parts = Rp / 256 + 1;
   }
   float* loss_dst = (out && out->loss) ? out->loss : c->loss_tmp;
-  // the loss sum runs beside the weight-gradient kernels
-  if ((rc = fork_side(c, 1, [&]() {
+  // the loss sum: inside the gradient finalize when that is tilefin_kernel,
+  // else its own launch
+  const bool loss_in_fin = grad && c->tnw;
+  if (!loss_in_fin && (rc = fork_side(c, 1, [&]() {
          RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, c->stream>>>(c->loss_part, nloss_parts, loss_dst));
          return DBSDE_OK;
        })))
@@ -1683,7 +1686,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     // ---- parameter gradients
     if (c->tnw) {
       if ((rc = launch_tnw(c, R, Rp))) return rc;
-      if ((rc = finalize_grads(c, params, grad))) return rc;
+      if ((rc = finalize_grads(c, params, grad, c->loss_part, nloss_parts, loss_dst))) return rc;
     } else {
     TNArgs ta;
     memset(&ta, 0, sizeof(ta));

@@ -852,9 +852,24 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
 // grid (ceil(T*T / 256), P + 1): y = P zero-fills the nslab == 0 windows.
 constexpr int TF_ELEMS = 256;   // elements per block (64 lanes x float4)
 __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int ndesc, const float* slab, int S,
-                                                      int P, int T, float* grad) {
+                                                      int P, int T, float* grad, const double* loss_part, int nloss,
+                                                      float* loss) {
   const int p = blockIdx.y;
   if (p == P) {   // zero windows (NAIS-Net's never-used input_layers[K])
+    // and, in block 0, the loss sum (loss_final_kernel's fixed order: one
+    // launch fewer on the step's critical path)
+    if (loss && blockIdx.x == 0) {
+      __shared__ double red[256];
+      double a = 0.0;
+      for (int i = threadIdx.x; i < nloss; i += 256) a += loss_part[i];
+      red[threadIdx.x] = a;
+      __syncthreads();
+      for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) loss[0] = (float)red[0];
+    }
     for (int i = 0; i < ndesc; ++i) {
       const PackDesc& d = descs[i];
       if (d.nslab != 0) continue;
