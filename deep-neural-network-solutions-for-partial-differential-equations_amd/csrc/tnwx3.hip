@@ -15,7 +15,7 @@
 // MFMA register form), the split B operands of the step (84 VGPRs), the raw
 // next step (112) and two split A blocks in VGPRs; the next step's loads are
 // issued a whole step (294 MFMAs) ahead, and every A split runs between the
-// MFMAs of the previous block (x3_product).
+// MFMAs of the previous block (x3_products).
 #include "tnw.hpp"
 
 namespace dbsde {
@@ -64,21 +64,29 @@ __device__ __forceinline__ void load_cols(float (&r)[NB][8], const float* X, int
   }
 }
 
-// acc += A[rows]^T B[rows] over 32-row steps [g0, g1).  Per step: the B
-// split (VALU) and the next step's B loads, then one scheduling region per
-// A block m: its 42 MFMAs with the split of A block m + 1 interleaved one
-// VALU per MFMA gap, and the next step's loads of A block m + 1.  The regions
-// are pinned (sched_barrier): left alone, the scheduler sinks the next step's
-// loads to the top of the next trip, right before their use.
+// acc += A1[rows]^T B1[rows] + A2[rows]^T B2[rows] over 32-row steps
+// [g0, g1) of both products as one pipeline of 2 (g1 - g0) steps (the second
+// product's first loads are in flight during the first product's last step).
+// Per step: the B split (VALU) and the next step's B loads, then one
+// scheduling region per A block m: its 42 MFMAs with the split of A block
+// m + 1 interleaved one VALU per MFMA gap, and the next step's loads of A block
+// m + 1.  The regions are pinned (sched_barrier): left alone, the scheduler
+// sinks the next step's loads to the top of the next trip, right before their
+// use.
 template <int NB>
-__device__ __forceinline__ void x3_product(floatx4 (&acc)[NB][NB], const float* A, int lda, const float* B, int ldb,
-                                           int g0, int g1, int i, int q) {
+__device__ __forceinline__ void x3_products(floatx4 (&acc)[NB][NB], const TNWProb& pr, int g0, int g1, int i, int q) {
+  const int n = g1 - g0, last = 2 * n - 1;
   float ra[NB][8], rb[NB][8];
-  load_cols<NB>(rb, B, ldb, 32 * g0 + 8 * q, i);
-  load_cols<NB>(ra, A, lda, 32 * g0 + 8 * q, i);
+  load_cols<NB>(rb, pr.B1, pr.ldb1, 32 * g0 + 8 * q, i);
+  load_cols<NB>(ra, pr.A1, pr.lda1, 32 * g0 + 8 * q, i);
   Split3 sa = split8(ra[0]);   // A block 0 of the step (the last region splits the next step's)
-  for (int g = g0; g < g1; ++g) {
-    const int nrow = 32 * min(g + 1, g1 - 1) + 8 * q;   // clamped prefetch, unused past the slice
+  for (int k = 0; k <= last; ++k) {
+    // the next step (clamped prefetch, unused past the end): product and row
+    const int kn = min(k + 1, last), second = kn >= n;
+    const float* A = second ? pr.A2 : pr.A1;
+    const float* B = second ? pr.B2 : pr.B1;
+    const int lda = second ? pr.lda2 : pr.lda1, ldb = second ? pr.ldb2 : pr.ldb1;
+    const int nrow = 32 * (g0 + (second ? kn - n : kn)) + 8 * q;
     Split3 sb[NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) sb[n] = split8(rb[n]);
@@ -142,8 +150,7 @@ __global__ void __launch_bounds__(256, 1) tnw_x3_kernel(TNWArgs a) {
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
   if (c1 > c0) {
-    x3_product<NB>(acc, pr.A1, pr.lda1, pr.B1, pr.ldb1, c0, c1, i, q);
-    x3_product<NB>(acc, pr.A2, pr.lda2, pr.B2, pr.ldb2, c0, c1, i, q);
+    x3_products<NB>(acc, pr, c0, c1, i, q);
   }
 #pragma unroll
   for (int m = 0; m < NB; ++m)
