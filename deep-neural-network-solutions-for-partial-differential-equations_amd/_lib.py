@@ -20,15 +20,18 @@ G_KINDS = {"sumsq": 0, "call_sum": 1, "call_mean": 2, "log": 3, "smooth_call": 4
 PROBLEM_KINDS = {"diag": 0, "heston": 1}
 OPTIMIZERS = {"Adam": 0, "AdamW": 1, "SGD": 2, "RMSprop": 3, "Adagrad": 4, "Adamax": 5, "Adadelta": 6, "ASGD": 7}
 EXACT_KINDS = {"bsb": 0, "bs_call": 1, "basket_avg": 2, "basket_mean": 3}
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # every symbol include/dbsde.h declares (checked by the CPU test suite)
 EXPORTED = [
     "dbsde_abi_version", "dbsde_create", "dbsde_destroy", "dbsde_last_error", "dbsde_set_stream",
     "dbsde_param_count", "dbsde_param_used_mask", "dbsde_matrix_form", "dbsde_brownian_dim", "dbsde_set_corr", "dbsde_brownian", "dbsde_prefetch",
+    "dbsde_prefetch_cancel",
     "dbsde_loss_grad", "dbsde_net_u", "dbsde_optimizer_step", "dbsde_exact", "dbsde_hjb_mc",
     "dbsde_profile_enable", "dbsde_profile_count", "dbsde_profile_read", "dbsde_profile_reset",
+    "dbsde_vec_reduce", "dbsde_vec_axpby", "dbsde_lbfgs_direction",
 ]
+VEC_OPS = {"dot": 0, "asum": 1, "amax": 2}
 
 
 class Problem(ctypes.Structure):
@@ -63,7 +66,8 @@ class Optim(ctypes.Structure):
                 ("beta2", ctypes.c_float), ("eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
                 ("max_norm", ctypes.c_float), ("step", ctypes.c_longlong), ("alpha", ctypes.c_float),
                 ("rho", ctypes.c_float), ("lr_decay", ctypes.c_float), ("lambd", ctypes.c_float),
-                ("asgd_eta", ctypes.c_float), ("asgd_mu", ctypes.c_float), ("loss", ctypes.c_void_p)]
+                ("asgd_eta", ctypes.c_float), ("asgd_mu", ctypes.c_float), ("loss", ctypes.c_void_p),
+                ("step_state", ctypes.c_void_p), ("step_parity", ctypes.c_int)]
 
 
 _LIB = None
@@ -92,6 +96,7 @@ def load():
         "dbsde_set_corr": (i, [vp, vp, i]),
         "dbsde_brownian": (i, [vp, ctypes.POINTER(Batch), vp, vp, i]),
         "dbsde_prefetch": (i, [vp, ctypes.POINTER(Batch)]),
+        "dbsde_prefetch_cancel": (i, [vp]),
         "dbsde_exact": (i, [i, vp, vp, ll, i, ctypes.c_float, vp, vp, vp, vp]),
         "dbsde_hjb_mc": (i, [vp, vp, i, i, ctypes.c_float, ll, ctypes.c_ulonglong, vp, vp]),
         "dbsde_loss_grad": (i, [vp, vp, ctypes.POINTER(Batch), vp, ctypes.POINTER(Outputs)]),
@@ -103,6 +108,9 @@ def load():
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ll)]),
         "dbsde_profile_reset": (i, [vp]),
+        "dbsde_vec_reduce": (i, [vp, i, vp, vp, ll, ctypes.POINTER(ctypes.c_double)]),
+        "dbsde_vec_axpby": (i, [vp, vp, vp, vp, ll, ctypes.c_float, ctypes.c_float]),
+        "dbsde_lbfgs_direction": (i, [vp, vp, vp, vp, ll, ll, vp, vp, i, ctypes.c_float, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -26,6 +26,7 @@
 #include "paths.hpp"
 #include "phase.hpp"
 #include "tnw.hpp"
+#include "vec.hpp"
 
 using namespace dbsde;
 
@@ -74,7 +75,9 @@ struct dbsde_ctx {
     bool valid = false;
     dbsde_batch b{};
     hipEvent_t ready = nullptr;
+    unsigned long long seq = 0;   // issue order: the older pending slot is the one replaced / reused
   } pend[2];
+  unsigned long long pf_seq = 0;
   hipStream_t pf_stream = nullptr;
   hipEvent_t ev_pf_order = nullptr;
   // path-chunked phase pipeline: chunk i runs phase A then phase C on stream
@@ -132,6 +135,7 @@ struct dbsde_ctx {
   std::vector<int> slab_mt, slab_nt, slab_mv, slab_nv;
   double* opt_part = nullptr;
   int opt_nparts = 0;
+  double* vec_part = nullptr;     // L-BFGS reductions: VEC_RED_BLOCKS partials + the result
 
   // ---- row buffers (grow with Rp)
   int cap_rows = 0, cap_n = 0;
@@ -435,7 +439,6 @@ inline float* gtag(long long off) { return (float*)(kGradTag | (uintptr_t)(off *
 int build_buffers(dbsde_ctx* c) {
   const int K = c->K, D = c->D, Dp = c->Dp;
   int rc;
-  if (const char* e = getenv("DBSDE_TN_SPLITS")) c->tn_splits = std::max(1, std::min(TN_SPLITS_MAX, atoi(e)));
   if ((rc = dalloc_t(c, &c->BtIn, (size_t)c->Stot_x * Dp))) return rc;
   if ((rc = dalloc_t(c, &c->BtZ, (size_t)Dp * c->Stot_x))) return rc;
   if ((rc = dalloc_t(c, &c->wout, (size_t)c->Wp[K]))) return rc;
@@ -564,7 +567,6 @@ int build_buffers(dbsde_ctx* c) {
   // P = 2K + 2 problems in 4-wave workgroups: K odd
   c->tnw = c->has_v && uniformW && c->Wp[0] == Dp && Dp <= 128 && K <= 6 && (2 * K + 2) % 4 == 0;
   if (const char* e = getenv("DBSDE_TNW")) c->tnw = c->tnw && atoi(e) != 0;
-  if (const char* e = getenv("DBSDE_TNW_SPLITS")) c->tnw_S = std::max(8, std::min(1024, atoi(e) / 8 * 8));
   std::vector<PackDesc> F;
   if (c->tnw) {
     const int T = Dp, P = 2 * K + 2, S = c->tnw_S;
@@ -838,9 +840,9 @@ int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
         from_pf = true;
       }
   if (use < 0) {
-    use = c->pend[0].valid ? (c->pend[1].valid ? 0 : 1) : 0;
-    // both pending and neither is this batch: the older one's buffer is reused
-    // once its rollout is done
+    // a buffer no prefetch holds; both pending and neither is this batch: the
+    // older one's buffer is reused once its rollout is done
+    use = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
     if (c->pend[use].valid) HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
   } else {
     HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
@@ -1399,10 +1401,6 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pf_order, hipEventDisableTiming);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pend[i].ready, hipEventDisableTiming);
-    if (const char* ch = getenv("DBSDE_CHUNKS")) c->chunks = std::max(1, std::min(16, atoi(ch)));
-    if (const char* ch = getenv("DBSDE_CHUNK0")) c->chunk0 = atoi(ch);
-    if (const char* ch = getenv("DBSDE_PIPES")) c->pipes = std::max(2, std::min(4, atoi(ch)));
-    if (const char* ch = getenv("DBSDE_SERIAL")) c->serial = atoi(ch);
     if (e != hipSuccess) rc = fail(c, DBSDE_EHIP, std::string("side stream: ") + hipGetErrorString(e));
   }
   if (rc) {
@@ -1854,10 +1852,71 @@ int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, flo
   }
   a.loss = o->loss;
   a.nparts = c->opt_nparts;
+  if (o->step_state) {
+    if (o->step_parity != 0 && o->step_parity != 1) return fail(c, DBSDE_EINVAL, "step_parity must be 0 or 1");
+    a.state = o->step_state;
+    a.parity = o->step_parity;
+    a.lr_d = o->lr;
+    a.beta1_d = o->beta1;
+    a.beta2_d = o->beta2;
+    a.lr_decay_d = o->lr_decay;
+    a.lambd_d = o->lambd;
+    a.asgd_alpha_d = 0.75;   // torch.optim.ASGD defaults (alpha, t0)
+    a.asgd_t0_d = 1e6;
+  }
   if (o->max_norm > 0.f)
     RUN(c, "grad_sqnorm", 2.0 * n, 4.0 * n, sqnorm_kernel<<<c->opt_nparts, 256, 0, s>>>(grad, c->d_used, n, c->opt_part));
   RUN(c, "optimizer", 10.0 * n, 24.0 * n,
       optim_kernel<<<256, 256, 0, s>>>(params, grad, m, v, c->d_used, n, c->opt_part, a));
+  return DBSDE_OK;
+}
+
+int dbsde_vec_reduce(dbsde_ctx* c, int op, const float* a, const float* b, long long n, double* result) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (op < DBSDE_VEC_DOT || op > DBSDE_VEC_AMAX || !a || (op == DBSDE_VEC_DOT && !b) || n < 1 || !result)
+    return fail(c, DBSDE_EINVAL, "bad dbsde_vec_reduce arguments");
+  HIPC(c, hipSetDevice(c->device));
+  int rc;
+  if (!c->vec_part && (rc = dalloc_t(c, &c->vec_part, VEC_RED_BLOCKS + 1))) return rc;
+  hipStream_t s = c->stream;
+  RUN(c, "vec_reduce", 2.0 * n, 8.0 * n, vec_reduce_kernel<<<VEC_RED_BLOCKS, 256, 0, s>>>(op, a, b, n, c->vec_part));
+  RUN(c, "vec_reduce", 0.0, 0.0,
+      vec_reduce_final_kernel<<<1, 256, 0, s>>>(op, c->vec_part, VEC_RED_BLOCKS, c->vec_part + VEC_RED_BLOCKS));
+  HIPC(c, hipMemcpyAsync(result, c->vec_part + VEC_RED_BLOCKS, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPC(c, hipStreamSynchronize(s));
+  return DBSDE_OK;
+}
+
+int dbsde_vec_axpby(dbsde_ctx* c, float* z, const float* x, const float* y, long long n, float alpha, float beta) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!z || !x || n < 1 || (!y && beta != 0.f)) return fail(c, DBSDE_EINVAL, "bad dbsde_vec_axpby arguments");
+  HIPC(c, hipSetDevice(c->device));
+  const unsigned blocks = (unsigned)std::min<long long>((n + 255) / 256, 1024);
+  RUN(c, "vec_axpby", 3.0 * n, 12.0 * n, vec_axpby_kernel<<<blocks, 256, 0, c->stream>>>(z, x, y, n, alpha, beta));
+  return DBSDE_OK;
+}
+
+int dbsde_lbfgs_direction(dbsde_ctx* c, const float* g, const float* S, const float* Y, long long ld, long long n,
+                          const int* slot, const float* ro, int num, float h_diag, float* d) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!g || !d || n < 1 || num < 0 || num > LBFGS_HMAX || (num > 0 && (!S || !Y || !slot || !ro || ld < n)))
+    return fail(c, DBSDE_EINVAL, "bad dbsde_lbfgs_direction arguments (at most 128 history entries)");
+  HIPC(c, hipSetDevice(c->device));
+  LbfgsArgs a{};
+  a.g = g;
+  a.S = S;
+  a.Y = Y;
+  a.ld = ld;
+  a.n = n;
+  a.d = d;
+  a.num = num;
+  a.h_diag = h_diag;
+  for (int i = 0; i < num; ++i) {
+    if (slot[i] < 0) return fail(c, DBSDE_EINVAL, "negative history slot");
+    a.slot[i] = slot[i];
+    a.ro[i] = ro[i];
+  }
+  RUN(c, "lbfgs_direction", 8.0 * n * num, 16.0 * n * num, lbfgs_direction_kernel<<<1, 1024, 0, c->stream>>>(a));
   return DBSDE_OK;
 }
 
@@ -1901,9 +1960,9 @@ int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
   if ((rc = ensure_rows(c, Rp, N))) return rc;
   for (int i = 0; i < 2; ++i)
     if (c->pend[i].valid && same_batch(c->pend[i].b, *next)) return DBSDE_OK;   // already queued
-  // a buffer no pending prefetch holds (else the first one's is replaced: its
+  // a buffer no pending prefetch holds (else the older one's is replaced: its
   // rollout is earlier on the same stream)
-  const int j = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : 0);
+  const int j = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
   // after everything queued so far on the caller's stream (Xi ready, the
   // buffer's previous readers done); work queued later overlaps this
   HIPC(c, hipEventRecord(c->ev_pf_order, c->stream));
@@ -1928,6 +1987,21 @@ int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
   HIPC(c, hipEventRecord(c->pend[j].ready, c->pf_stream));
   c->pend[j].valid = true;
   c->pend[j].b = *next;
+  c->pend[j].seq = ++c->pf_seq;
+  return DBSDE_OK;
+}
+
+int dbsde_prefetch_cancel(dbsde_ctx* c) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  HIPC(c, hipSetDevice(c->device));
+  // the pending rollouts still run to completion; their buffers are just not
+  // matched any more (and are not rewritten before they are done: the stream
+  // that reuses a buffer waits for the prefetch stream)
+  if (c->pf_stream) {
+    HIPC(c, hipEventRecord(c->ev_pf_order, c->pf_stream));
+    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_pf_order, 0));
+  }
+  c->pend[0].valid = c->pend[1].valid = false;
   return DBSDE_OK;
 }
 

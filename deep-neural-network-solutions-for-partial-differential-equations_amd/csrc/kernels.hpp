@@ -23,44 +23,19 @@ enum Act { ACT_SINE = 0, ACT_RELU = 1, ACT_TANH = 2 };
 // sin and cos together on the transcendental unit: a is reduced modulo 2*pi in
 // radians (two-part Cody-Waite 2*pi in fp32, |r| <= pi), scaled to revolutions
 // and fed to v_sin_f32 / v_cos_f32 (sin(2*pi*x), quarter rate).  7 VALU-slot
-// equivalents per element instead of ~25 for the polynomial below; the phase
+// equivalents per element instead of ~25 for a minimax polynomial; the phase
 // kernels evaluate it 4 (phase A) and 8 (phase C) times per activation element.
 // Max abs error ~3e-7 (2.5 ulp of 1), independent of |a| because the
 // reduction happens before the scaling (tools/ubench/sincos_acc.hip measures
 // it against fp64 libm on the GPU; the plain fract-of-a/(2pi) form grows to
-// 5.5e-6 at |a| = 64).  DBSDE_SINCOS_POLY selects the polynomial (A/B only).
+// 5.5e-6 at |a| = 64).
 __device__ __forceinline__ void fast_sincosf(float a, float& s, float& c) {
-#ifndef DBSDE_SINCOS_POLY
   const float k = rintf(a * 0.15915494309189535f);
   float r = fmaf(-k, 6.2831854820251465f, a);   // 2pi_hi = fp32(2pi)
   r = fmaf(-k, -1.7484555314695172e-07f, r);    // 2pi_lo = 2pi - 2pi_hi
   const float rev = r * 0.15915494309189535f;   // [-1/2, 1/2]
   s = __builtin_amdgcn_sinf(rev);
   c = __builtin_amdgcn_cosf(rev);
-#else
-  // Cody-Waite reduction with a 3-part pi/2 in fp32 for |a| <= 8192 (fp64
-  // reduction above), cephes minimax polynomials in fp32 on [-pi/4, pi/4];
-  // max abs error < 0.8 * 2^-23 for |a| <= 2e4.
-  float r;
-  int m;
-  if (__builtin_expect(fabsf(a) <= 8192.f, 1)) {
-    const float k = rintf(a * 0.636619772367581f);
-    r = fmaf(-k, 1.5707963705062866f, a);
-    r = fmaf(-k, -4.371138828673793e-08f, r);
-    r = fmaf(-k, -1.7763568394002505e-15f, r);
-    m = (int)k & 3;
-  } else {
-    const double k = rint((double)a * 0.63661977236758134308);
-    r = (float)fma(-k, 1.5707963267948966192, (double)a);
-    m = (int)(long long)k & 3;
-  }
-  const float z = r * r;
-  const float sp = r + r * z * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
-  const float cp =
-      1.0f - 0.5f * z + z * z * (4.166664568298827e-2f + z * (-1.388731625493765e-3f + z * 2.443315711809948e-5f));
-  s = (m == 0) ? sp : (m == 1) ? cp : (m == 2) ? -sp : -cp;
-  c = (m == 0) ? cp : (m == 1) ? -sp : (m == 2) ? -cp : sp;
-#endif
 }
 __device__ __forceinline__ float act_f(int act, float a) {
   if (act == ACT_SINE) {
@@ -676,12 +651,38 @@ struct OptArgs {
   float asgd_mu;
   const float* loss;          // nullable: skip the whole update when the loss is not finite
   int nparts;
+  // device step counter (nullable): the step-dependent scalars above are then
+  // derived on the device from step = state[parity] + 1, and the count advances
+  // (state[1 - parity]) only when the update is not skipped
+  double* state;
+  int parity;
+  double lr_d, beta1_d, beta2_d, lr_decay_d, lambd_d, asgd_alpha_d, asgd_t0_d;
 };
+
+// torch.optim's Python-float scalars of update number t (torch 2.10
+// single-tensor paths): Adam/AdamW/Adamax bias corrections, Adagrad's clr and
+// ASGD's eta / mu, which torch computes after step t - 1 and keeps as fp32
+__device__ inline void opt_step_scalars(OptArgs& a, double t) {
+  const double bc1 = 1.0 - pow(a.beta1_d, t), bc2 = 1.0 - pow(a.beta2_d, t);
+  a.step_size = (float)(a.lr_d / bc1);
+  a.bc2_sqrt = (float)sqrt(bc2);
+  if (a.kind == OPT_ADAGRAD) a.step_size = (float)(a.lr_d / (1.0 + (t - 1.0) * a.lr_decay_d));
+  if (a.kind == OPT_ASGD) {
+    const double tp = t - 1.0;   // eta / mu were set by the previous step (lr and 1 before the first)
+    const float eta = tp < 1.0 ? (float)a.lr_d : (float)(a.lr_d / pow(1.0 + a.lambd_d * a.lr_d * tp, a.asgd_alpha_d));
+    const float mu = tp < 1.0 ? 1.f : (float)(1.0 / fmax(1.0, tp - a.asgd_t0_d));
+    a.asgd_eta = eta;
+    a.asgd_decay = (float)(1.0 - a.lambd_d * (double)eta);
+    a.asgd_mu = mu;
+    a.asgd_copy = mu == 1.f;
+  }
+}
 
 __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float* m, float* v, const unsigned char* used,
                                                     long long n, const double* part, OptArgs a) {
   __shared__ float clip_s;
   __shared__ int skip_s;
+  __shared__ OptArgs a_s;
   if (threadIdx.x == 0) {
     float coef = 1.f;
     if (a.max_norm > 0.f) {
@@ -692,10 +693,19 @@ __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float*
       if (coef > 1.f) coef = 1.f;
     }
     clip_s = coef;
-    skip_s = a.loss ? !isfinite(a.loss[0]) : 0;   // heston_dnnpde.py:409-411 NaN skip
+    const int skip = a.loss ? !isfinite(a.loss[0]) : 0;   // heston_dnnpde.py:409-411 NaN skip
+    skip_s = skip;
+    if (a.state) {
+      // every block reads state[parity]; only block 0 writes the other slot
+      const double done = a.state[a.parity];
+      opt_step_scalars(a, done + 1.0);
+      if (blockIdx.x == 0) a.state[1 - a.parity] = skip ? done : done + 1.0;
+    }
+    a_s = a;
   }
   __syncthreads();
   if (skip_s) return;
+  a = a_s;
   const float coef = clip_s;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     if (!used[i]) continue;

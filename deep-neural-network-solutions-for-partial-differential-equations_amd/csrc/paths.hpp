@@ -200,10 +200,14 @@ __global__ void __launch_bounds__(256) rollout_corr_kernel(RolloutArgs p) {
     x[i] = ok[i] ? p.Xi[(p.xi_rows == 1 ? 0 : mi[i]) * p.D + d] : 0.f;
   }
   double tacc = 0.0;
-  float t0 = 0.f;
+  // time grid: the caller's t [M, N+1] when given (as step_block), else the
+  // reference's fp32(fp64 cumsum of T/N)
+  float t0[CP_PPT];
 #pragma unroll
-  for (int i = 0; i < CP_PPT; ++i)
-    if (ok[i] && p.out != PATH_ROLLOUT) fa[i].put(p, mi[i], d, 0, 0.f, 0.f);
+  for (int i = 0; i < CP_PPT; ++i) {
+    t0[i] = (p.t && ok[i]) ? p.t[(size_t)mi[i] * N1] : 0.f;
+    if (ok[i] && p.out != PATH_ROLLOUT) fa[i].put(p, mi[i], d, 0, t0[i], 0.f);
+  }
   int buf = 0;
   for (int n0 = 0; n0 < p.N; n0 += 4) {
     float z[CP_PPT][4];
@@ -219,7 +223,9 @@ __global__ void __launch_bounds__(256) rollout_corr_kernel(RolloutArgs p) {
         for (int i = 0; i < CP_PPT; ++i) zs[(buf * nb + d) * PB + grp * CP_PPT + i] = sqdt * z[i][k4];
       }
       tacc += dt64;
-      const float t1 = (float)tacc;
+      float t1[CP_PPT];
+#pragma unroll
+      for (int i = 0; i < CP_PPT; ++i) t1[i] = (p.t && ok[i]) ? p.t[(size_t)mi[i] * N1 + n + 1] : (float)tacc;
       __syncthreads();
       float acc[CP_PPT] = {};
       if (active_d) {
@@ -238,23 +244,24 @@ __global__ void __launch_bounds__(256) rollout_corr_kernel(RolloutArgs p) {
       for (int i = 0; i < CP_PPT; ++i) {
         if (!ok[i]) continue;
         if (p.out != PATH_ROLLOUT) {
-          fa[i].put(p, mi[i], d, n + 1, t1, acc[i]);
+          fa[i].put(p, mi[i], d, n + 1, t1[i], acc[i]);
           continue;
         }
         const size_t r = (size_t)mi[i] * N1 + n;
         float* xr = p.xin + r * p.ldx;
         xr[1 + d] = x[i];
         if (d == 0) {
-          xr[0] = t0;
+          xr[0] = t0[i];
           xr[p.D + 1] = 1.0f;
         }
-        const float dt = rn_sub(t1, t0);
+        const float dt = rn_sub(t1[i], t0[i]);
         const float sg = rn_add(rn_mul(p.sig_a, x[i]), p.sig_b);
         const float s = rn_mul(sg, acc[i]);
         p.sdw[r * p.ldx + 1 + d] = s;
         x[i] = rn_add(rn_add(x[i], rn_mul(rn_mul(p.mu_a, x[i]), dt)), s);
       }
-      t0 = t1;
+#pragma unroll
+      for (int i = 0; i < CP_PPT; ++i) t0[i] = t1[i];
     }
   }
   if (p.out != PATH_ROLLOUT) return;
@@ -266,7 +273,7 @@ __global__ void __launch_bounds__(256) rollout_corr_kernel(RolloutArgs p) {
     xr[1 + d] = x[i];
     p.sdw[r * p.ldx + 1 + d] = 0.0f;
     if (d == 0) {
-      xr[0] = t0;
+      xr[0] = t0[i];
       xr[p.D + 1] = 1.0f;
     }
   }

@@ -183,12 +183,7 @@ struct PieceStagerT {
   const float* const* img;
   const int* nf;
   int n, st, wave, lane, buf;
-#ifdef DBSDE_STAMPS   // diagnostic build (tools/exp_phase.py stamps): per-piece s_memtime
-  unsigned long long ts[3 * 64];
-  __device__ __forceinline__ void mark() { ts[3 * (st - 1) + 2] = __builtin_amdgcn_s_memtime(); }
-#else
   __device__ __forceinline__ void mark() {}
-#endif
   __device__ __forceinline__ void start() {
 #pragma unroll
     for (int k = 0; k < NBUF - 1; ++k)
@@ -196,9 +191,6 @@ struct PieceStagerT {
   }
   template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
-#ifdef DBSDE_STAMPS
-    ts[3 * st] = __builtin_amdgcn_s_memtime();
-#endif
     if constexpr (NBUF > 2) {
       if (st + 1 < n)
         vm_wait<NYOUNG + LC>();
@@ -208,9 +200,6 @@ struct PieceStagerT {
       vm_wait<NYOUNG>();
     }
     lds_barrier();
-#ifdef DBSDE_STAMPS
-    ts[3 * st + 1] = __builtin_amdgcn_s_memtime();
-#endif
     constexpr int DIST = NBUF - 1;
     if (st + DIST < n) piece_dma(img[st + DIST], nf[st + DIST], wl + ((st + DIST) % NBUF) * buf, wave, lane);
     // nothing issued later may be hoisted above the DMA (the NYOUNG counts)
@@ -224,21 +213,6 @@ struct PieceStagerT {
 template <bool X3, int T, int TD>
 using PieceStager = PieceStagerT<X3 ? 3 : 2, X3 ? (3 * (T < TD ? T : TD)) / P3_WAVES : 0>;
 
-#ifdef DBSDE_STAMPS
-template <class SG>
-__device__ __forceinline__ void stamp_dump(const SG& sg, char kind, int tile) {
-  const unsigned long long tend = __builtin_amdgcn_s_memtime();
-  if ((tile == 5 || tile == 405 || tile == 805) && (threadIdx.x & 63) == 0)
-    for (int i = 0; i < sg.n; ++i) {
-      const unsigned long long nx = i + 1 < sg.n ? sg.ts[3 * i + 3] : tend;
-      printf("STAMP %c %d %d %d wait %llu mfma %llu post %llu\n", kind, tile, sg.wave, i, sg.ts[3 * i + 1] - sg.ts[3 * i],
-             sg.ts[3 * i + 2] - sg.ts[3 * i + 1], nx - sg.ts[3 * i + 2]);
-    }
-}
-#define STAMP_DUMP(kind) stamp_dump(sg, kind, tile)
-#else
-#define STAMP_DUMP(kind)
-#endif
 
 struct NoOp {
   __device__ __forceinline__ void operator()() const {}
@@ -575,7 +549,6 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseA_kernel(FusedArgs p) {
     *(floatx4*)o = floatx4{v6[0], v6[1], v6[2], v6[3]};
     *(floatx4*)(o + 4) = floatx4{v6[4], v6[5], umask, 0.f};
   }
-  STAMP_DUMP('A');
 }
 
 // ---------------------------------------------------------------------------
@@ -724,7 +697,6 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseC_kernel(FusedArgs p) {
       }
   });
   bstore_stream(al, p.Alpha, S, row0, 0);
-  STAMP_DUMP('C');
 }
 
 }  // namespace dbsde

@@ -34,41 +34,15 @@ __device__ __forceinline__ void tnw_mma(floatx4 (&acc)[NB][NB], const TnwStage<N
 }
 
 // acc += A[rows]^T B[rows] over k-steps [g0, g1), g1 - g0 a positive
-// multiple of 4: four-stage register pipeline, steps g+1..g+3 in flight while
+// multiple of 4: three-stage register ring, steps g+1, g+2 in flight while
 // step g is multiplied.  The loop body has no branches (prefetches past the
 // slice are clamped to its last step and never used), so the accumulators
 // stay in place and the waitcnts only cover the stage being consumed.
-#ifndef TNW_STAGES
-#define TNW_STAGES 3
-#endif
 template <int NB>
 __device__ __forceinline__ void tnw_product(floatx4 (&acc)[NB][NB], const float* A, int lda, const float* B, int ldb,
                                             int g0, int g1, int i, int kq) {
-  TnwStage<NB> q0, q1, q2, q3;
+  TnwStage<NB> q0, q1, q2;
   const int gl = g1 - 1;
-#if TNW_STAGES == 4
-  tnw_load<NB>(A, lda, B, ldb, 4 * g0 + kq, i, q0);
-  tnw_load<NB>(A, lda, B, ldb, 4 * (g0 + 1) + kq, i, q1);
-  tnw_load<NB>(A, lda, B, ldb, 4 * (g0 + 2) + kq, i, q2);
-  for (int g = g0; g < g1; g += 4) {
-    tnw_load<NB>(A, lda, B, ldb, 4 * (g + 3) + kq, i, q3);
-    __builtin_amdgcn_sched_barrier(0);
-    tnw_mma<NB>(acc, q0);
-    __builtin_amdgcn_sched_barrier(0);
-    tnw_load<NB>(A, lda, B, ldb, 4 * min(g + 4, gl) + kq, i, q0);
-    __builtin_amdgcn_sched_barrier(0);
-    tnw_mma<NB>(acc, q1);
-    __builtin_amdgcn_sched_barrier(0);
-    tnw_load<NB>(A, lda, B, ldb, 4 * min(g + 5, gl) + kq, i, q1);
-    __builtin_amdgcn_sched_barrier(0);
-    tnw_mma<NB>(acc, q2);
-    __builtin_amdgcn_sched_barrier(0);
-    tnw_load<NB>(A, lda, B, ldb, 4 * min(g + 6, gl) + kq, i, q2);
-    __builtin_amdgcn_sched_barrier(0);
-    tnw_mma<NB>(acc, q3);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#else
   // three-stage ring with a 3-step body (fixed rotation), then a 0-2 step tail
   tnw_load<NB>(A, lda, B, ldb, 4 * g0 + kq, i, q0);
   tnw_load<NB>(A, lda, B, ldb, 4 * (g0 + 1) + kq, i, q1);
@@ -89,22 +63,14 @@ __device__ __forceinline__ void tnw_product(floatx4 (&acc)[NB][NB], const float*
   }
   if (g < g1) tnw_mma<NB>(acc, q0);
   if (g + 1 < g1) tnw_mma<NB>(acc, q1);
-  (void)q3;
-#endif
 }
-
-#if defined(DBSDE_TNW_WPE1)
-#define TNW_OCC __attribute__((amdgpu_waves_per_eu(1, 1)))
-#else
-#define TNW_OCC
-#endif
 
 // One workgroup = four waves = four problems of the same row slice: the four
 // waves land on the four SIMDs of a CU, so the placement of the long-running
 // waves is even.  XCD-aware mapping: the P/4 workgroups of a slice share
 // blockIdx % 8.
 template <int NB>
-__global__ void __launch_bounds__(256, 1) TNW_OCC tnw_kernel(TNWArgs a) {
+__global__ void __launch_bounds__(256, 1) tnw_kernel(TNWArgs a) {
   const int wg = blockIdx.x, wpg = a.P / 4;
   const int xcd = wg & 7, local = wg >> 3;
   const int s = (local / wpg) * 8 + xcd;

@@ -31,7 +31,7 @@ from . import networks
 from .solver import NativeSolver, ProblemSpec
 
 OPTIMIZER_NAMES = ("Adam", "SGD", "RMSprop", "AdamW", "Adadelta", "Adagrad", "Adamax", "ASGD", "LBFGS")
-NATIVE_OPTIMIZERS = ("Adam", "SGD", "RMSprop", "AdamW", "Adadelta", "Adagrad", "Adamax", "ASGD")
+NATIVE_OPTIMIZERS = OPTIMIZER_NAMES
 # torch.optim defaults of each optimizer as the reference builds it, optim.X(params, lr=lr)
 # (nd_BSPDE_case.py:331-350; torch 2.10 signatures)
 OPT_DEFAULTS = {
@@ -65,7 +65,9 @@ class FBSNN(ABC):
     clip_max_norm = 1.0          # nd_BSPDE_case.py:383 (DeepBSDE: none)
     schedule = "nd"              # Q1: "nd" (nd_BSPDE_case.py:364-368), "corr" (with_corr:406-409) or None
     skip_nonfinite = False       # heston_dnnpde.py:409-411 skips an iteration whose loss is NaN
-    log_every = 100
+    log_every = 100              # nd_BSPDE_case.py:395,402 (with_corr / hjb: 500)
+    log_print = True             # nd / hjb print the logged iterations (with_corr's print is commented out)
+    train_returns_time_logs = False   # with_corr...py:453, hjb_implement.py:450 return 4 values
 
     def __init__(self, Xi, T, M, N, D, Mm, layers, mode, activation, correlation_type="no_correlation",
                  device=None):
@@ -261,43 +263,135 @@ class FBSNN(ABC):
     def _check_optimizer(self, optimizer_type):
         if optimizer_type not in OPTIMIZER_NAMES:
             raise ValueError(f"Optimizer type '{optimizer_type}' is not recognized.")
-        if optimizer_type not in NATIVE_OPTIMIZERS:
-            raise NotImplementedError(f"optimizer {optimizer_type!r} has no native implementation yet "
-                                      f"(available: {', '.join(NATIVE_OPTIMIZERS)})")
 
     def new_optimizer_state(self, optimizer_type="Adam", learning_rate=None):
         """A fresh optimizer (the reference builds one per train() call, Q11)."""
         self._check_optimizer(optimizer_type)
-        st = {"kind": optimizer_type, "lr": learning_rate, "m": torch.zeros_like(self.params),
-              "v": torch.zeros_like(self.params), "step": 0}
-        if optimizer_type == "ASGD":      # torch keeps eta and mu as fp32 state tensors
-            st["eta"] = float(np.float32(learning_rate if learning_rate is not None else 0.0))
-            st["mu"] = 1.0
-        return st
+        if optimizer_type == "LBFGS":
+            return self._lbfgs_state(learning_rate)
+        # "dstep": the update count lives on the device (dbsde_optim.step_state),
+        # so an update skipped for a non-finite loss does not advance Adam's bias
+        # corrections or ASGD's eta / mu (heston_dnnpde.py:409-411 skips before
+        # optimizer.step()); "calls" counts the launches (ping-pong slot)
+        return {"kind": optimizer_type, "lr": learning_rate, "m": torch.zeros_like(self.params),
+                "v": torch.zeros_like(self.params), "dstep": torch.zeros(2, dtype=torch.float64, device=self.device),
+                "calls": 0}
 
     def _update(self, opt, learning_rate=None, skip_loss=None):
         """clip_grad_norm_ (not for LBFGS) + optimizer.step() on the device."""
         kind = opt["kind"]
+        if kind == "LBFGS":
+            raise ValueError("LBFGS steps need a closure (FBSNN._lbfgs_step)")
         lr = opt["lr"] if learning_rate is None else learning_rate
-        if kind == "ASGD" and opt["step"] == 0 and opt["lr"] is None:
-            opt["eta"] = float(np.float32(lr))
         kw = OPT_DEFAULTS[kind]
-        opt["step"] += 1
+        parity = opt["calls"] & 1
+        opt["calls"] += 1
         self.solver.optimizer_step(
             self.params, self.grad, opt["m"], opt["v"], kind=kind, lr=lr, betas=kw.get("betas", (0.9, 0.999)),
             eps=kw.get("eps", 1e-8), weight_decay=kw["weight_decay"], max_norm=self.clip_max_norm or 0.0,
-            step=opt["step"], alpha=kw.get("alpha", 0.99) if kind == "RMSprop" else 0.99, rho=kw.get("rho", 0.9),
-            lr_decay=kw.get("lr_decay", 0.0), lambd=kw.get("lambd", 1e-4), asgd_eta=opt.get("eta", 0.0),
-            asgd_mu=opt.get("mu", 1.0), skip_nonfinite_loss=skip_loss)
-        if kind == "ASGD":                # torch.optim.asgd: eta / mu of the next step
-            t = float(opt["step"])
-            opt["eta"] = float(np.float32(lr / ((1 + kw["lambd"] * lr * t) ** kw["alpha"])))
-            opt["mu"] = float(np.float32(1 / max(1, t - kw["t0"])))
+            step=opt["calls"], alpha=kw.get("alpha", 0.99) if kind == "RMSprop" else 0.99, rho=kw.get("rho", 0.9),
+            lr_decay=kw.get("lr_decay", 0.0), lambd=kw.get("lambd", 1e-4), skip_nonfinite_loss=skip_loss,
+            step_state=opt["dstep"], step_parity=parity)
+
+    def optimizer_steps_taken(self, opt):
+        """Updates the device has applied (skipped ones excluded); syncs."""
+        return int(opt["dstep"][opt["calls"] & 1].item())
+
+    # ------------------------------------------------------------------ L-BFGS
+    def _lbfgs_state(self, lr):
+        """torch.optim.LBFGS(params, lr) with its defaults (nd_BSPDE_case.py:347-348):
+        max_iter 20, max_eval 25, tolerance_grad 1e-7, tolerance_change 1e-9,
+        history_size 100, no line search.  The history lives in two device
+        matrices of history_size + 1 rows (one scratch row for the candidate
+        pair before torch's ys > 1e-10 test)."""
+        n = self.params.numel()
+        H = 100
+        z = lambda *shape: torch.zeros(*shape, device=self.device)   # noqa: E731
+        return {"kind": "LBFGS", "lr": 1.0 if lr is None else lr, "max_iter": 20, "max_eval": 25,
+                "tolerance_grad": 1e-7, "tolerance_change": 1e-9, "history_size": H,
+                "S": z(H + 1, n), "Y": z(H + 1, n), "slots": [], "ro": [], "free": list(range(H + 1)),
+                "d": z(n), "prev_g": z(n), "t": None, "H_diag": 1.0, "prev_loss": None, "n_iter": 0,
+                "func_evals": 0}
+
+    def _lbfgs_step(self, st, closure):
+        """torch.optim.LBFGS.step(closure) (torch 2.10, line_search_fn=None)
+        restated: the same control flow and fp32 scalars, every vector
+        operation on the device (dbsde_vec_reduce / dbsde_vec_axpby /
+        dbsde_lbfgs_direction).  closure() re-runs the native loss and gradient
+        into self.grad on the same batch and returns the loss as a float.
+        Returns the loss of the first evaluation (torch's orig_loss)."""
+        sv, g, d, f32 = self.solver, self.grad, st["d"], np.float32
+        lr, tol_grad, tol_change = st["lr"], st["tolerance_grad"], st["tolerance_change"]
+        orig_loss = closure()
+        loss = orig_loss
+        current_evals = 1
+        st["func_evals"] += 1
+        if sv.vec_reduce("amax", g) <= tol_grad:
+            return orig_loss
+        t = st["t"]
+        n_iter = 0
+        while n_iter < st["max_iter"]:
+            n_iter += 1
+            st["n_iter"] += 1
+            if st["n_iter"] == 1:
+                sv.vec_axpby(d, g, -1.0)                                   # d = -g
+                st["slots"], st["ro"], st["H_diag"] = [], [], 1.0
+                st["free"] = list(range(st["history_size"] + 1))
+            else:
+                c = st["free"][0]
+                y, s = st["Y"][c], st["S"][c]
+                sv.vec_axpby(y, g, 1.0, st["prev_g"], -1.0)                # y = g - prev_g
+                sv.vec_axpby(s, d, float(f32(t)))                          # s = d * t
+                ys = f32(sv.vec_reduce("dot", y, s))
+                if ys > 1e-10:
+                    if len(st["slots"]) == st["history_size"]:
+                        st["free"].append(st["slots"].pop(0))
+                        st["ro"].pop(0)
+                    st["free"].remove(c)
+                    st["slots"].append(c)
+                    st["ro"].append(float(f32(1.0) / ys))
+                    st["H_diag"] = float(ys / f32(sv.vec_reduce("dot", y, y)))
+                sv.lbfgs_direction(g, st["S"], st["Y"], st["slots"], st["ro"], st["H_diag"], d)
+            sv.vec_axpby(st["prev_g"], g, 1.0)
+            prev_loss = loss
+            if st["n_iter"] == 1:
+                inv = f32(1.0) / f32(sv.vec_reduce("asum", g))
+                t = float(f32(inv * f32(lr))) if inv < 1.0 else 1.0 * lr
+            else:
+                t = lr
+            gtd = f32(sv.vec_reduce("dot", g, d))
+            if gtd > -tol_change:
+                break
+            ls_func_evals = 0
+            sv.vec_axpby(self.params, d, float(f32(t)), self.params, 1.0)   # _add_grad(t, d)
+            opt_cond = False
+            if n_iter != st["max_iter"]:
+                loss = closure()
+                opt_cond = sv.vec_reduce("amax", g) <= tol_grad
+                ls_func_evals = 1
+            current_evals += ls_func_evals
+            st["func_evals"] += ls_func_evals
+            if n_iter == st["max_iter"] or current_evals >= st["max_eval"] or opt_cond:
+                break
+            if f32(sv.vec_reduce("amax", d)) * abs(f32(t)) <= tol_change:
+                break
+            if abs(loss - prev_loss) < tol_change:
+                break
+        st["t"] = t
+        st["prev_loss"] = prev_loss
+        return orig_loss
 
     def _reduce(self):
         if self.world > 1:
             dist.all_reduce(self._gradbuf)     # RCCL over xGMI: [grad | loss], ~0.37 MB
         return self._gradbuf[-1:]
+
+    def _closure(self, t, W, p0, ml, M):
+        """The reference's LBFGS closure (nd_BSPDE_case.py:357-361): loss and
+        gradient again on the same batch; returns the (all-reduced) loss."""
+        self._run(t[p0:p0 + ml], W[p0:p0 + ml], self._local_xi(p0, ml, M), grad=self.grad, want=(),
+                  loss=self._gradbuf[-1:])
+        return float(self._reduce().item())
 
     def train_step(self, t, W, opt_state, optimizer_type=None, learning_rate=None, want_state=False):
         """loss/grad on the local shard of a global minibatch (t, W: host numpy
@@ -308,8 +402,31 @@ class FBSNN(ABC):
         out = self._run(t[p0:p0 + ml], W[p0:p0 + ml], self._local_xi(p0, ml, M), grad=self.grad,
                         want=("X", "Y") if want_state else (), loss=self._gradbuf[-1:])
         loss = self._reduce()
+        if opt_state["kind"] == "LBFGS":
+            loss = loss.clone()
+            self._lbfgs_step(opt_state, lambda: self._closure(t, W, p0, ml, M))
+            return loss, out
         self._update(opt_state, learning_rate, skip_loss=loss if self.skip_nonfinite else None)
         return loss, out
+
+    def _device_xi(self, p0, ml):
+        """The persistent device copy of this shard's Xi that device-mode batches
+        (and their prefetch, which matches on the pointer) read.  It is
+        refreshed whenever self.Xi is replaced or modified in place (tensor
+        version counter), so a changed Xi is never served from a stale copy."""
+        src = self.Xi
+        key = (p0, ml, self.M, id(src), getattr(src, "_version", None))
+        if getattr(self, "_xi_dev_key", None) != key:
+            xi = self._local_xi(p0, ml, self.M)
+            if getattr(self, "_xi_dev", None) is not None and self._xi_dev.shape == xi.shape:
+                # the pending prefetch read the old values: drop it before rewriting
+                self.solver.prefetch_drop()
+                self._xi_dev.copy_(xi)
+            else:
+                self._xi_dev = xi.clone()
+            self._xi_dev_src = src          # keeps id(src) from being reused while cached
+            self._xi_dev_key = key
+        return self._xi_dev
 
     def device_step(self, opt_state, learning_rate=None, seed=0, optimizer_type=None, next_seed=None):
         """Throughput-mode iteration: Brownian increments drawn on the device
@@ -321,22 +438,29 @@ class FBSNN(ABC):
         if self._L is not None and self.spec.kind != "diag":
             raise NotImplementedError("device-mode correlated increments are implemented for diagonal problems")
         p0, ml = self._local_slice(self.M)
-        key = (p0, ml, self.M, self.N, id(self.Xi))
-        if getattr(self, "_xi_dev_key", None) != key:   # one Xi tensor per shard (the prefetch matches its pointer)
-            self._xi_dev = self._local_xi(p0, ml, self.M).clone()
-            self._xi_dev_key = key
-        xi = self._xi_dev
-        if next_seed is not None:
+        xi = self._device_xi(p0, ml)
+        lbfgs = opt_state["kind"] == "LBFGS"
+        if next_seed is not None and not lbfgs:
             self.solver.prefetch(ml, self.N, xi, seed=next_seed, path0=p0)
         self.solver.loss_grad(self.params, ml, self.N, xi, seed=seed, path0=p0,
                               grad=self.grad, loss=self._gradbuf[-1:])
         loss = self._reduce()
+        if lbfgs:
+            def closure():
+                self.solver.loss_grad(self.params, ml, self.N, xi, seed=seed, path0=p0, grad=self.grad,
+                                      loss=self._gradbuf[-1:])
+                return float(self._reduce().item())
+            loss = loss.clone()
+            self._lbfgs_step(opt_state, closure)
+            return loss
         self._update(opt_state, learning_rate, skip_loss=loss if self.skip_nonfinite else None)
         return loss
 
     def train_device(self, N_Iter, learning_rate, seed=0, optimizer_type="Adam"):
         """train() with device-generated Brownian increments (no numpy stream,
-        no per-iteration host sync except every log_every iterations)."""
+        no per-iteration host sync except every log_every iterations).  Like
+        the reference's NaN skip (heston_dnnpde.py:409-411), non-finite losses
+        are left out of the logged window means."""
         previous_it = self.iteration[-1] if self.iteration else 0
         opt_state = self.new_optimizer_state(optimizer_type, learning_rate)
         losses = []
@@ -345,7 +469,10 @@ class FBSNN(ABC):
             nxt = (seed << 20) + it + 1 if it + 1 < previous_it + N_Iter else None
             losses.append(self.device_step(opt_state, learning_rate, seed=(seed << 20) + it, next_seed=nxt).clone())
             if it % self.log_every == 0:
-                self.training_loss.append(float(torch.cat(losses).mean()))
+                window = torch.cat(losses)
+                if self.skip_nonfinite:
+                    window = window[torch.isfinite(window)]
+                self.training_loss.append(float(window.mean()) if window.numel() else float("nan"))
                 losses = []
                 self.iteration.append(it)
         return np.stack((self.iteration, self.training_loss))
@@ -357,11 +484,17 @@ class FBSNN(ABC):
         return np.stack((self.iteration, self.training_loss))
 
     def train(self, N_Iter, learning_rate, optimizer_type='Adam'):
-        """nd_BSPDE_case.py:316-410 -> (graph, min_loss, min_loss_state)."""
+        """nd_BSPDE_case.py:316-410 -> (graph, min_loss, min_loss_state); the
+        with_corr / hjb classes (train_returns_time_logs) log every 500
+        iterations and also return time_logs (with_corr...py:355-453,
+        hjb_implement.py:394-450).  LBFGS runs optimizer.step(closure) with the
+        native loss as the closure and no clipping, as the reference does."""
         opt_state = self.new_optimizer_state(optimizer_type, learning_rate)   # fresh per call (Q11)
+        lbfgs = optimizer_type == "LBFGS"
         loss_temp = []
         previous_it = self.iteration[-1] if self.iteration else 0
         start_time = time.time()
+        cumulative_time, time_logs = 0.0, []
         min_loss, min_loss_state = float('inf'), None
         for it in range(previous_it, previous_it + N_Iter):
             self._schedule_n(it)
@@ -374,14 +507,19 @@ class FBSNN(ABC):
             if self.skip_nonfinite and not np.isfinite(loss):
                 print(f"NaN loss detected at iteration {it}. Skipping this iteration")
                 continue
-            self._update(opt_state, learning_rate)
+            if lbfgs:
+                self._lbfgs_step(opt_state, lambda: self._closure(t_np, W_np, p0, ml, M))
+            else:
+                self._update(opt_state, learning_rate)
             loss_temp.append(loss)
             if loss < min_loss:
                 min_loss = loss
                 min_loss_state = (out["X"].clone(), out["Y"].clone())
             if it % self.log_every == 0:
                 elapsed = time.time() - start_time
-                if self.rank == 0:
+                cumulative_time += elapsed
+                time_logs.append(cumulative_time)
+                if self.rank == 0 and self.log_print:
                     y0 = float(out["Y"][0, 0, 0])
                     print(f'It: {it}, Loss: {loss:.3e}, Y0: {y0:.3f}, Time: {elapsed:.2f}, '
                           f'Learning Rate: {learning_rate:.3e}')
@@ -390,6 +528,8 @@ class FBSNN(ABC):
                 loss_temp = []
                 self.iteration.append(it)
                 self._record_y0(out)
+        if self.train_returns_time_logs:
+            return self._train_graph(), min_loss, min_loss_state, time_logs
         return self._train_graph(), min_loss, min_loss_state
 
     # ------------------------------------------------------------------ inference

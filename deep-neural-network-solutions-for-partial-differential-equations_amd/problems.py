@@ -62,11 +62,20 @@ class CallOption1D(FBSNN):
         return 0.25 * torch.diag_embed(X)
 
 
-class BasketCallOption(FBSNN):
-    """with_corr_high_dimension_pde.py:546-596 (its FBSNN sets strike = 1.0 and
-    applies the N**(1/5) schedule of with_corr...:406-409)."""
+class _WithCorrTrain:
+    """The train() surface of with_corr_high_dimension_pde.py:355-453: log and
+    record every 500 iterations (no print), return (graph, min_loss,
+    min_loss_state, time_logs)."""
 
     schedule = "corr"
+    log_every = 500
+    log_print = False
+    train_returns_time_logs = True
+
+
+class BasketCallOption(_WithCorrTrain, FBSNN):
+    """with_corr_high_dimension_pde.py:546-596 (its FBSNN sets strike = 1.0 and
+    applies the N**(1/5) schedule of with_corr...:406-409)."""
 
     def _default_strike(self):
         return 1.0
@@ -87,10 +96,8 @@ class BasketCallOption(FBSNN):
         return 0.20 * torch.diag_embed(X)
 
 
-class BSPDETestCase(FBSNN):
+class BSPDETestCase(_WithCorrTrain, FBSNN):
     """with_corr_high_dimension_pde.py:599-616."""
-
-    schedule = "corr"
 
     def _default_strike(self):
         return 1.0
@@ -113,7 +120,12 @@ class BSPDETestCase(FBSNN):
 
 class HamiltonJacobiBellman(FBSNN):
     """hjb_implement.py:590-604.  The reference passes Mm=None and therefore
-    cannot train (np.ceil(None)); here Mm=None means a fixed N."""
+    cannot train (np.ceil(None)); here Mm=None means a fixed N.
+    Its train() (hjb_implement.py:394-450) logs and prints every 500
+    iterations and returns (graph, min_loss, min_loss_state, time_logs)."""
+
+    log_every = 500
+    train_returns_time_logs = True
 
     def __init__(self, Xi, T, M, N, D, layers, mode, activation, **kw):
         super().__init__(Xi, T, M, N, D, None, layers, mode, activation, **kw)
@@ -150,6 +162,7 @@ class HestonFBSNN(FBSNN):
     reference golden; k = 1 is pinned by tests/golden/g1_heston_*."""
 
     skip_nonfinite = True
+    log_print = False             # its progress print is commented out (heston_dnnpde.py:432-434)
 
     def __init__(self, Xi, T, M, N, D, Mm, layers, mode, activation, correlation_type="no_correlation",
                  kappa=2.0, theta=0.2, sigma=0.3, rho=0.8, v0=0.2, payoff_type='discontinuous', device=None):
@@ -172,13 +185,16 @@ class HestonFBSNN(FBSNN):
         return networks.make_heston_model(self.mode, layers, self.activation, 1 + 2 * self.n_assets)
 
     def _full_state(self, Xi):
-        """[S_1..S_k] (or the reference's [S]) -> [S_1..S_k, v0..v0]."""
+        """[S_1..S_k, ...] -> [S_1..S_k, v0..v0]: the reference always starts the
+        variance at self.v0 and reads only the S column(s) of Xi
+        (heston_dnnpde.py:619-623; predict may append v0, :668-670, which
+        loss_function then ignores)."""
         k = self.n_assets
         x = torch.as_tensor(np.asarray(Xi) if not isinstance(Xi, torch.Tensor) else Xi,
                             dtype=torch.float32).to(self.device)
         x = x.reshape(-1, x.shape[-1]) if x.dim() > 1 else x.reshape(1, -1)
-        if x.shape[1] == 2 * k:
-            return x.contiguous()
+        if x.shape[1] < k:
+            raise ValueError(f"Xi has {x.shape[1]} columns; the {k} asset prices come first")
         S = x[:, :k]
         return torch.cat([S, torch.full_like(S, self.v0)], 1).contiguous()
 

@@ -153,6 +153,11 @@ class NativeSolver:
         self._bind_stream()
         _lib.check(self.lib.dbsde_prefetch(self.ctx, ctypes.byref(b)), self.ctx)
 
+    def prefetch_drop(self):
+        """Forget pending prefetches (dbsde_prefetch_cancel)."""
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_prefetch_cancel(self.ctx), self.ctx)
+
     def net_u(self, params, t, X, u, Du):
         R = X.numel() // self.D
         self._check_tensor(params, "params", self.nparams)
@@ -164,20 +169,64 @@ class NativeSolver:
 
     def optimizer_step(self, params, grad, m, v, kind="Adam", lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
                        weight_decay=0.0, max_norm=0.0, step=1, alpha=0.99, rho=0.9, lr_decay=0.0, lambd=1e-4,
-                       asgd_eta=0.0, asgd_mu=1.0, skip_nonfinite_loss=None):
+                       asgd_eta=0.0, asgd_mu=1.0, skip_nonfinite_loss=None, step_state=None, step_parity=0):
         """clip_grad_norm_ + optimizer.step() over the flat parameters; m, v are
-        the optimizer's state buffers (see include/dbsde.h DBSDE_OPT_*)."""
+        the optimizer's state buffers (see include/dbsde.h DBSDE_OPT_*).
+        step_state: optional device float64[2] step counter (dbsde_optim.step_state):
+        the update number, and from it the step-dependent scalars, then come from
+        the device, and a skipped update does not advance it."""
         if kind not in _lib.OPTIMIZERS:
             raise ValueError(f"Optimizer type '{kind}' is not recognized.")
         for name, v_ in (("params", params), ("grad", grad), ("m", m), ("v", v)):
             self._check_tensor(v_, name, self.nparams)
         self._check_tensor(skip_nonfinite_loss, "loss", 1)
+        if step_state is not None and (step_state.device != self.device or step_state.dtype != torch.float64
+                                       or step_state.numel() != 2):
+            raise ValueError(f"step_state must be a float64 tensor of 2 elements on {self.device}")
         o = _lib.Optim(_lib.OPTIMIZERS[kind], lr, betas[0], betas[1], eps, weight_decay,
                        max_norm if max_norm else 0.0, int(step), alpha, rho, lr_decay, lambd, asgd_eta, asgd_mu,
-                       _ptr(skip_nonfinite_loss))
+                       _ptr(skip_nonfinite_loss), _ptr(step_state), int(step_parity))
         self._bind_stream()
         _lib.check(self.lib.dbsde_optimizer_step(self.ctx, _ptr(params), _ptr(grad), _ptr(m), _ptr(v),
                                                  ctypes.byref(o)), self.ctx)
+
+    # ------------------------------------------------------------------ L-BFGS vector primitives
+    def vec_reduce(self, op, a, b=None):
+        """Fixed-order fp64 sum a.b ("dot"), sum |a| ("asum") or max |a| ("amax")
+        of device fp32 vectors, returned as a Python float (syncs)."""
+        self._check_tensor(a, "a")
+        self._check_tensor(b, "b", a.numel() if b is not None else None)
+        out = ctypes.c_double()
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_vec_reduce(self.ctx, _lib.VEC_OPS[op], _ptr(a), _ptr(b), a.numel(),
+                                             ctypes.byref(out)), self.ctx)
+        return out.value
+
+    def vec_axpby(self, z, x, alpha, y=None, beta=0.0):
+        """z = alpha x + beta y (fp32, on the device)."""
+        for name, v in (("z", z), ("x", x), ("y", y)):
+            self._check_tensor(v, name, z.numel() if v is not None else None)
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_vec_axpby(self.ctx, _ptr(z), _ptr(x), _ptr(y), z.numel(), float(alpha),
+                                            float(beta)), self.ctx)
+
+    def lbfgs_direction(self, g, S, Y, slots, ro, h_diag, d):
+        """torch LBFGS two-loop recursion over history rows `slots` (oldest first)."""
+        n = g.numel()
+        for name, v in (("g", g), ("d", d)):
+            self._check_tensor(v, name, n)
+        num = len(slots)
+        if num:
+            self._check_tensor(S, "S")
+            self._check_tensor(Y, "Y", S.numel())
+            if S.dim() != 2 or S.shape[1] < n or max(slots) >= S.shape[0]:
+                raise ValueError("history matrices must be [slots, >= n] and hold every slot")
+        sl = (ctypes.c_int * max(num, 1))(*slots)
+        rv = (ctypes.c_float * max(num, 1))(*ro)
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_lbfgs_direction(self.ctx, _ptr(g), _ptr(S) if num else None,
+                                                  _ptr(Y) if num else None, S.shape[1] if num else n, n, sl, rv,
+                                                  num, float(h_diag), _ptr(d)), self.ctx)
 
     # ------------------------------------------------------------------ Brownian increments
     def set_corr(self, L):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DBSDE_ABI_VERSION 2
+#define DBSDE_ABI_VERSION 3
 
 /* error codes */
 #define DBSDE_OK 0
@@ -195,6 +195,10 @@ int dbsde_brownian(dbsde_ctx* ctx, const dbsde_batch* batch, float* t, float* W,
  * this call.  dbsde_set_corr drops pending prefetches.
  */
 int dbsde_prefetch(dbsde_ctx* ctx, const dbsde_batch* next);
+/* Forget every pending prefetch (e.g. the caller is about to rewrite the Xi
+ * buffer a prefetch read); later batches roll out as usual.  The context stream
+ * is ordered after the pending rollouts, so their buffers are reused safely. */
+int dbsde_prefetch_cancel(dbsde_ctx* ctx);
 
 /*
  * FBSNN.loss_function + loss.backward (DeepBSDE.py:202-245, 279).
@@ -233,12 +237,46 @@ typedef struct dbsde_optim {
   float asgd_mu;     /* state; the caller runs that recursion                   */
   const float* loss; /* nullable device scalar: skip the update when it is not
                         finite (heston_dnnpde.py:409-411 NaN skip)              */
+  /* nullable device double[2]: the optimizer's step count kept on the device,
+     so that a skipped update does not advance it (the reference `continue`s
+     before optimizer.step(), heston_dnnpde.py:409-411).  When set, the update
+     reads the completed step count from step_state[step_parity], runs update
+     number count + 1 (bias corrections, Adagrad's clr, ASGD's eta / mu derived
+     on the device from it; `step`, asgd_eta and asgd_mu are ignored) and writes
+     the new count -- the old one when skipped -- to step_state[1 - step_parity].
+     Successive calls alternate step_parity. */
+  double* step_state;
+  int step_parity;
 } dbsde_optim;
 
 /* clip_grad_norm_ + optimizer.step() (nd_BSPDE_case.py:383-384); m, v device
  * flat state owned by the caller (zero-initialised for a fresh optimizer). */
 int dbsde_optimizer_step(dbsde_ctx* ctx, float* params, float* grad, float* m, float* v,
                          const dbsde_optim* opt);
+
+/*
+ * L-BFGS (torch.optim.LBFGS(params, lr) as nd_BSPDE_case.py:347-348 and
+ * with_corr...py:386-387 build it; train() calls optimizer.step(closure) with a
+ * closure that re-runs loss_function + backward on the same batch, without
+ * clipping: nd_BSPDE_case.py:357-361,380-381).  The closure is dbsde_loss_grad;
+ * the host runs torch's step logic (fbsnn.py) on these device-vector
+ * primitives.  Vectors are device fp32 of n elements (the flat parameter
+ * order); reductions are fixed-order fp64, returned to the host (they
+ * synchronise the context stream).
+ */
+#define DBSDE_VEC_DOT 0    /* sum_i a_i b_i */
+#define DBSDE_VEC_ASUM 1   /* sum_i |a_i|   (b unused) */
+#define DBSDE_VEC_AMAX 2   /* max_i |a_i|   (b unused) */
+int dbsde_vec_reduce(dbsde_ctx* ctx, int op, const float* a, const float* b, long long n, double* result);
+/* z = alpha x + beta y in fp32 (z may alias x or y; y may be NULL when beta == 0) */
+int dbsde_vec_axpby(dbsde_ctx* ctx, float* z, const float* x, const float* y, long long n, float alpha, float beta);
+/* The L-BFGS two-loop recursion (torch's LBFGS.step direction), one launch:
+ *   q = -g; for i = num-1..0: al_i = (s_i.q) ro_i, q -= al_i y_i;
+ *   d = q h_diag; for i = 0..num-1: be_i = (y_i.d) ro_i, d += (al_i - be_i) s_i
+ * s_i / y_i = rows slot[i] of the device [*, ld] history matrices S / Y (oldest
+ * first, num <= 128); slot and ro are host arrays. */
+int dbsde_lbfgs_direction(dbsde_ctx* ctx, const float* g, const float* S, const float* Y, long long ld, long long n,
+                          const int* slot, const float* ro, int num, float h_diag, float* d);
 
 /*
  * Exact / comparator solutions on the device (the references' evaluators):

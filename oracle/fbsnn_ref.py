@@ -384,24 +384,43 @@ def loss_and_grads(model, problem, t, W, Xi, M, D):
 
 
 def train(model, problem, Xi, M, N, D, T, n_iter, lr, clip=True, Mm=None,
-          start_it=0, L=None, rng=None):
+          start_it=0, L=None, rng=None, schedule="nd", optimizer="Adam"):
     """nd_BSPDE_case.py:316-410 (clip=True, Mm schedule) or DeepBSDE.py:265-295
-    (clip=False, Mm=None).  A fresh Adam per call (Q11).  Returns per-iteration
+    (clip=False, Mm=None); schedule="corr" is with_corr...py:405-409 (N**(1/5)
+    re-applied to the mutated N).  A fresh optimizer per call (Q11);
+    optimizer="LBFGS" runs optimizer.step(closure) on the same batch without
+    clipping (nd_BSPDE_case.py:357-361,380-381).  Returns per-iteration
     (loss, Y0) lists."""
-    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    if optimizer == "LBFGS":
+        opt = torch.optim.LBFGS(model.parameters(), lr=lr)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=lr)
     Xi_t = torch.as_tensor(Xi, dtype=torch.float32)
     losses, y0s = [], []
     for it in range(start_it, start_it + n_iter):
-        if Mm is not None:
+        if schedule == "corr":
+            if 4000 <= it < 20000:
+                N = int(np.ceil((N ** (1 / 5)) ** (int(it / 4000) + 1)))
+            elif it < 4000:
+                N = int(np.ceil(N ** (1 / 5)))
+        elif Mm is not None:
             N = n_schedule(it, Mm, N)
         opt.zero_grad()
         t, W = fetch_minibatch(M, N, D, T, L=L, rng=rng)
         xi = Xi_t.clone().requires_grad_(True)
         loss, X, Y, y0, _ = loss_function(model, problem, t, W, xi, M, D)
         loss.backward()
-        if clip:
-            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
-        opt.step()
+        if optimizer == "LBFGS":
+            def closure():
+                opt.zero_grad()
+                l2 = loss_function(model, problem, t, W, Xi_t.clone().requires_grad_(True), M, D)[0]
+                l2.backward()
+                return l2
+            opt.step(closure)
+        else:
+            if clip:
+                torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+            opt.step()
         losses.append(float(loss))
         y0s.append(y0)
     return losses, y0s

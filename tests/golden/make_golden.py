@@ -369,8 +369,86 @@ def north_star_trajectory(mods, seed=0, steps=(1, 10, 100)):
     np.savez_compressed(os.path.join(OUT, "g2_north_star_trajectory.npz"), **out)
 
 
+def round3_cases(mods):
+    """Round 3: (a) the hv = false split-bf16 kernels at the north-star width --
+    FC-Sine and Resnet-Sine [101,110x4,1] on DeepBSDE's BSB (DeepBSDE.py:166-178);
+    (b) the with_corr / hjb train() surface: 15 iterations from iteration 490,
+    crossing the it % 500 log (with_corr...py:355-453, hjb_implement.py:394-450;
+    the reference HJB passes Mm=None, which cannot train, so Mm is set to N);
+    (c) optimizer_type='LBFGS' through the nd train() (nd_BSPDE_case.py:347-348,
+    357-361, 380-381): the closure re-evaluates on the same batch, no clip."""
+    import torch
+    D = 100
+    L110 = [D + 1] + 4 * [110] + [1]
+    xi_bsb = np.array([1.0, 0.5] * (D // 2))[None, :]
+    for k, mode in enumerate(["FC", "Resnet"]):
+        seed = 500 + k
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        with contextlib.redirect_stdout(io.StringIO()):
+            obj = mods["deep"].BlackScholesBarenblatt(xi_bsb, 1.0, 16, 5, D, L110, mode, "Sine")
+        params = _flat(obj.model.state_dict())
+        res = _run_case(obj, 16, 5, D)
+        _save_case(f"w110_deep_bsb_{mode}_Sine", "bsb", mode, "Sine", L110, xi_bsb, 16, 5, seed, params, res)
+
+    D4 = 4
+    L4 = [D4 + 1, 16, 16, 16, 16, 1]
+    specs = [("train_it500_corr_basket_Naisnet_Sine", "corr", "CallOption", "basket", "Naisnet", "Sine",
+              np.ones((1, D4)), {"Mm": 5.0, "correlation_type": "random_correlation"}),
+             ("train_it500_hjb_Naisnet_Tanh", "hjb", "HamiltonJacobiBellman", "hjb", "Naisnet", "Tanh",
+              np.zeros((1, D4)), {})]
+    for k, (name, modkey, cls, prob, mode, act, Xi, kw) in enumerate(specs):
+        seed = 510 + k
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        C = getattr(mods[modkey], cls)
+        with contextlib.redirect_stdout(io.StringIO()):
+            if modkey == "corr":
+                obj = C(Xi, 1.0, 8, 5, D4, kw["Mm"], L4, mode, act, kw["correlation_type"])
+            else:
+                obj = C(Xi, 1.0, 8, 5, D4, L4, mode, act)
+                obj.Mm = 5.0                 # N = ceil(Mm) = 5 for it < 4000
+        corr = np.asarray(obj.correlation_matrix, np.float64)
+        obj.iteration = [490]
+        obj.training_loss = [1.25]
+        p0 = _flat(obj.model.state_dict())
+        np.random.seed(520 + k)
+        with contextlib.redirect_stdout(io.StringIO()):
+            graph, min_loss, state, time_logs = obj.train(15, 1e-3)
+        p1 = _flat(obj.model.state_dict())
+        np.savez_compressed(os.path.join(OUT, f"g1_{name}.npz"), name=name, problem=prob, mode=mode,
+                            activation=act, layers=np.array(L4), Xi=Xi.astype(np.float32), M=8, N=5, T=1.0,
+                            Mm=5.0, iters=15, lr=1e-3, batch_seed=520 + k, start_iteration=490, start_loss=1.25,
+                            params0=p0, params1=p1, graph=np.asarray(graph, np.float64), min_loss=np.float64(min_loss),
+                            min_X=state[0].numpy(), min_Y=state[1].numpy(), n_time_logs=len(time_logs),
+                            N_final=obj.N, corr=corr)
+        print(f"{name:42s} graph={np.asarray(graph).tolist()} min_loss={min_loss:.6e}", flush=True)
+
+    # LBFGS through the nd train(): 3 outer iterations (each up to 20 inner)
+    torch.manual_seed(530)
+    np.random.seed(530)
+    with contextlib.redirect_stdout(io.StringIO()):
+        obj = mods["nd"].CallOption(np.ones((1, D4)), 1.0, 8, 5, D4, 5.0, L4, "Naisnet", "Sine")
+    p0 = _flat(obj.model.state_dict())
+    np.random.seed(531)
+    with contextlib.redirect_stdout(io.StringIO()):
+        graph, min_loss, _ = obj.train(3, 0.05, optimizer_type="LBFGS")
+    p1 = _flat(obj.model.state_dict())
+    st = obj.optimizer.state[obj.optimizer._params[0]]
+    np.savez_compressed(os.path.join(OUT, "g1_train_lbfgs_nd_call_Naisnet_Sine.npz"),
+                        name="train_lbfgs_nd_call_Naisnet_Sine", problem="call", mode="Naisnet", activation="Sine",
+                        layers=np.array(L4), Xi=np.ones((1, D4), np.float32), M=8, N=5, T=1.0, Mm=5.0, iters=3,
+                        lr=0.05, batch_seed=531, params0=p0, params1=p1, min_loss=np.float64(min_loss),
+                        func_evals=int(st["func_evals"]), n_iter=int(st["n_iter"]))
+    print(f"{'train_lbfgs_nd_call_Naisnet_Sine':42s} |dp|={np.abs(p1 - p0).max():.3e} evals={st['func_evals']}",
+          flush=True)
+
+
 if __name__ == "__main__":
     m = _setup()
+    if "--round3-only" in sys.argv:
+        round3_cases(m)
+        sys.exit(0)
     if "--trajectory-only" in sys.argv:
         north_star_trajectory(m)
         sys.exit(0)

@@ -43,7 +43,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 def test_abi_version_and_config_validation(lib):
     pkg = load_pkg()
-    assert lib.dbsde_abi_version() == pkg._lib.ABI_VERSION == 2
+    assert lib.dbsde_abi_version() == pkg._lib.ABI_VERSION == 3
     cfg = pkg._lib.Config()
     cfg.mode, cfg.activation, cfg.n_layers = 1, 0, 2          # too few layers -> EINVAL before any HIP call
     ctx = ctypes.c_void_p()
@@ -76,6 +76,7 @@ int main(void) {
   F(dbsde_optim, max_norm) F(dbsde_optim, step) F(dbsde_problem, q3)
   F(dbsde_problem, kind) F(dbsde_problem, g_cols) F(dbsde_problem, u_clamp) F(dbsde_problem, h_rho)
   F(dbsde_optim, alpha) F(dbsde_optim, asgd_mu) F(dbsde_optim, loss)
+  F(dbsde_optim, step_state) F(dbsde_optim, step_parity)
   return 0;
 }
 '''
@@ -102,7 +103,8 @@ def test_struct_layouts_match_ctypes(tmp_path):
             "dbsde_problem.kind": L.Problem.kind, "dbsde_problem.g_cols": L.Problem.g_cols,
             "dbsde_problem.u_clamp": L.Problem.u_clamp, "dbsde_problem.h_rho": L.Problem.h_rho,
             "dbsde_optim.alpha": L.Optim.alpha, "dbsde_optim.asgd_mu": L.Optim.asgd_mu,
-            "dbsde_optim.loss": L.Optim.loss}
+            "dbsde_optim.loss": L.Optim.loss, "dbsde_optim.step_state": L.Optim.step_state,
+            "dbsde_optim.step_parity": L.Optim.step_parity}
     for k, field in offs.items():
         assert int(got[k]) == field.offset, k
 
