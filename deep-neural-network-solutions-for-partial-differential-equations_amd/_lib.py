@@ -29,7 +29,7 @@ EXPORTED = [
     "dbsde_prefetch_cancel",
     "dbsde_loss_grad", "dbsde_net_u", "dbsde_optimizer_step", "dbsde_exact", "dbsde_hjb_mc",
     "dbsde_profile_enable", "dbsde_profile_count", "dbsde_profile_read", "dbsde_profile_reset",
-    "dbsde_vec_reduce", "dbsde_vec_axpby", "dbsde_lbfgs_direction",
+    "dbsde_vec_reduce", "dbsde_vec_axpby", "dbsde_lbfgs_direction", "dbsde_train_step",
 ]
 VEC_OPS = {"dot": 0, "asum": 1, "amax": 2}
 
@@ -108,6 +108,8 @@ def load():
                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ll)]),
         "dbsde_profile_reset": (i, [vp]),
+        "dbsde_train_step": (i, [vp, vp, ctypes.POINTER(Batch), vp, vp, vp, ctypes.POINTER(Optim),
+                                 ctypes.POINTER(Outputs)]),
         "dbsde_vec_reduce": (i, [vp, i, vp, vp, ll, ctypes.POINTER(ctypes.c_double)]),
         "dbsde_vec_axpby": (i, [vp, vp, vp, vp, ll, ctypes.c_float, ctypes.c_float]),
         "dbsde_lbfgs_direction": (i, [vp, vp, vp, vp, ll, ll, vp, vp, i, ctypes.c_float, vp]),

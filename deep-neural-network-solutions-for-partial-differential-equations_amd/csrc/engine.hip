@@ -128,6 +128,7 @@ struct dbsde_ctx {
   unsigned char* d_used = nullptr;
   PackDesc* d_prep = nullptr;
   int n_prep = 0;
+
   int prep_blocks = 1;   // pack_tagged_kernel grid.x: one element per thread
   PackDesc* d_fin = nullptr;
   int n_fin = 0;
@@ -855,7 +856,7 @@ int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
 
 int prep_weights(dbsde_ctx* c, const float* params);
 int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double* loss_part = nullptr, int nloss = 0,
-                   float* loss = nullptr);
+                   float* loss = nullptr, const FusedOpt* fo = nullptr);
 
 }  // namespace
 
@@ -867,8 +868,8 @@ __device__ __forceinline__ const float* untag(const float* p, const float* param
   if (v & ((uintptr_t)1 << 61)) return grad + ((v & (((uintptr_t)1 << 61) - 1)) >> 2);
   return p;
 }
-__global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs, const float* params, float* grad) {
-  PackDesc d = descs[blockIdx.y];
+__device__ __forceinline__ void pack_block(const PackDesc* descs, int di, const float* params, float* grad) {
+  PackDesc d = descs[di];
   d.src = untag(d.src, params, grad);
   d.src2 = untag(d.src2, params, grad);
   d.dst = (float*)untag(d.dst, params, grad);
@@ -940,17 +941,20 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
     }
   }
 }
+__global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs, const float* params, float* grad) {
+  pack_block(descs, blockIdx.y, params, grad);
+}
 // RtR_j = W_j^T W_j (Functions/naisnet.py:33) and per-tile partial sums of
 // squares for the Frobenius norm (fixed order).  One 16x16 output tile per
 // 256-thread workgroup; the whole 16 x L and L x 16 operand strips (L <= 128)
 // are staged in LDS with one round of independent loads (a K-tiled loop would
 // chain L/16 dependent global-load latencies).
-__global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, const long long* woffs, int L,
-                                                         float* const* rtr, double* part, int nblk) {
+__device__ __forceinline__ void rtr_tile(const float* params, const long long* woffs, int L, float* const* rtr,
+                                         double* part, int nblk, int j, int tile) {
   __shared__ float As[16][NAIS_LMAX + 1];   // As[r][k] = W[k][16 ti + r]
   __shared__ float Bs[NAIS_LMAX][17];       // Bs[k][c] = W[k][16 tj + c]
-  const int j = blockIdx.y, nt = (L + 15) / 16;
-  const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
+  const int nt = (L + 15) / 16;
+  const int ti = tile / nt, tj = tile % nt;
   const float* W = params + woffs[j];
   for (int e = threadIdx.x; e < 16 * L; e += 256) {
     const int k = e >> 4, q = e & 15;
@@ -975,7 +979,11 @@ __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, co
     if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) part[j * nblk + blockIdx.x] = red[0];
+  if (threadIdx.x == 0) part[j * nblk + tile] = red[0];
+}
+__global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, const long long* woffs, int L,
+                                                         float* const* rtr, double* part, int nblk) {
+  rtr_tile(params, woffs, L, rtr, part, nblk, blockIdx.y, blockIdx.x);
 }
 // NAIS projection adjoint (Functions/naisnet.py:30-39 reversed), one kernel:
 //   Abar_j = dL/dA_j (slab sums), R_j = W_j^T W_j, n = |R_j|_F
@@ -987,12 +995,13 @@ __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, co
 // formed on the fly in the B tile of the LDS-tiled GEMM.
 __global__ void __launch_bounds__(256) proj_backward_kernel(const float* params, const long long* woffs,
                                                             float* const* abar, float* const* rtr, int L,
-                                                            const double* norms, const double* dot_part, int dot_nblk,
-                                                            int dot_nused,
-                                                            float* grad) {
+                                                            const double* proj_part, int proj_n, const double* dot_part,
+                                                            int dot_nblk, int dot_nused, float* grad, FusedOpt fo,
+                                                            int fuse) {
+  if (fuse) fused_opt_prologue(fo, false);
   __shared__ float As[16][NAIS_LMAX + 1];   // As[r][k] = W[16 ti + r][k]
   __shared__ float Bs[NAIS_LMAX][17];       // Bs[k][c] = S[k][16 tj + c], S = Rbar + Rbar^T
-  __shared__ double dot_s;
+  __shared__ double dot_s, nrm_s;
   const int j = blockIdx.y, nt = (L + 15) / 16;
   const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
   const float* Ab = abar[j];
@@ -1017,11 +1026,16 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* params,
     for (int b = threadIdx.x; b < dot_nused; b += 64) dsum += dot_part[(size_t)j * dot_nblk + b];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) dsum += __shfl_xor(dsum, o);
-    if (threadIdx.x == 0) dot_s = dsum;
+    // |R_j|_F from the rtr partials (proj_n <= 64), the phase kernels' order
+    const double nrm = nais_norm_from(threadIdx.x < proj_n ? proj_part[(size_t)j * proj_n + threadIdx.x] : 0.0);
+    if (threadIdx.x == 0) {
+      dot_s = dsum;
+      nrm_s = nrm;
+    }
   }
   __syncthreads();
   const double dot = dot_s;
-  const double n = norms[j];
+  const double n = nrm_s;
   const bool taken = (float)n > 0.98f;
   const float cA = taken ? (float)(0.98994949366116658 / sqrt(n)) : 1.f;
   const float cR = taken ? (float)(0.98994949366116658 / sqrt(n) * 0.5 * dot / (n * n)) : 0.f;
@@ -1039,7 +1053,11 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* params,
   const int row = ti * 16 + ty, col = tj * 16 + tx;
   float acc = 0.f;
   for (int k = 0; k < L; ++k) acc += As[ty][k] * Bs[k][tx];
-  if (row < L && col < L) grad[woffs[j] + row * L + col] = acc;
+  if (row < L && col < L) {
+    const long long i = woffs[j] + row * L + col;
+    grad[i] = acc;
+    if (fuse) opt_update(fo.a, i, acc, fo.prm, fo.m, fo.v);
+  }
 }
 }  // namespace dbsde
 
@@ -1117,13 +1135,18 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp) {
   return DBSDE_OK;
 }
 
-int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double* loss_part, int nloss, float* loss) {
+int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double* loss_part, int nloss, float* loss,
+                   const FusedOpt* fo) {
   hipStream_t s = c->stream;
+  FusedOpt fz{};
+  const FusedOpt& f = fo ? *fo : fz;
+  const int fuse = fo ? 1 : 0;
+  if (fo && !c->tnw) return fail(c, DBSDE_EINVAL, "internal: fused update needs the tile finalize");
   if (c->tnw) {
     const int T = c->Dp;
-    RUN(c, "grad_finalize", 0.0, 0.0,
+    RUN(c, fuse ? "grad_finalize_update" : "grad_finalize", 0.0, 0.0,
         tilefin_kernel<<<dim3((T * T + TF_ELEMS - 1) / TF_ELEMS, c->tnw_P + 1), 256, 0, s>>>(
-            c->d_fin, c->n_fin, c->slabW, c->tnw_S, c->tnw_P, T, grad, loss_part, nloss, loss));
+            c->d_fin, c->n_fin, c->slabW, c->tnw_S, c->tnw_P, T, grad, loss_part, nloss, loss, f, fuse));
   } else {
     RUN(c, "grad_finalize", 0.0, 0.0, slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad));
   }
@@ -1131,8 +1154,9 @@ int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double*
     const int LW = c->L[1];
     const int ntile = ((LW + 15) / 16) * ((LW + 15) / 16);
     RUN(c, "proj_backward", 2.0 * c->K * LW * (double)LW * LW, 0.0,
-        proj_backward_kernel<<<dim3(ntile, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_abar, c->d_rtr, LW, c->norms,
-                                                               c->dot_part, c->dot_nblk, c->dot_nused, grad));
+        proj_backward_kernel<<<dim3(ntile, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_abar, c->d_rtr, LW,
+                                                               c->proj_part, ntile, c->dot_part, c->dot_nblk,
+                                                               c->dot_nused, grad, f, fuse));
   }
   return DBSDE_OK;
 }
@@ -1305,6 +1329,7 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
   a.loss_part = c->loss_part;
   a.Hdot = c->Hdot;
   a.Alpha = c->Alpha;
+
   // stage sequences (phase.hpp): every image streamed as two pieces, input
   // blocks [0, H) and [H, TI)
   const int TW = c->Wp[0] / 16, TDp = c->Dp / 16, K = c->K;
@@ -1459,8 +1484,13 @@ int dbsde_param_used_mask(const dbsde_ctx* c, unsigned char* mask, long long n) 
   return DBSDE_OK;
 }
 
-int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, float* grad,
-                    const dbsde_outputs* out) {
+}  // extern "C"
+
+namespace {
+// dbsde_loss_grad, and dbsde_train_step's fused form (fo != NULL: the
+// optimizer update is applied inside the gradient finalize)
+int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, float* grad, const dbsde_outputs* out,
+                   const FusedOpt* fo) {
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
   if (!params) return fail(c, DBSDE_EINVAL, "params is NULL");
   int rc = validate_batch(c, b);
@@ -1684,7 +1714,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     // ---- parameter gradients
     if (c->tnw) {
       if ((rc = launch_tnw(c, R, Rp))) return rc;
-      if ((rc = finalize_grads(c, params, grad, c->loss_part, nloss_parts, loss_dst))) return rc;
+      if ((rc = finalize_grads(c, params, grad, c->loss_part, nloss_parts, loss_dst, fo))) return rc;
     } else {
     TNArgs ta;
     memset(&ta, 0, sizeof(ta));
@@ -1770,7 +1800,7 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
     }
     if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
     RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
-    if ((rc = finalize_grads(c, params, grad))) return rc;
+    if ((rc = finalize_grads(c, params, grad, nullptr, 0, nullptr, fo))) return rc;
     }
   }
 
@@ -1784,48 +1814,12 @@ int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, flo
   return DBSDE_OK;
 }
 
-int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const float* X, float* u, float* Du) {
-  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
-  if (!params || !t || !X || R < 1) return fail(c, DBSDE_EINVAL, "bad net_u arguments");
-  HIPC(c, hipSetDevice(c->device));
-  const int Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD, D = c->D;
-  int rc;
-  if ((rc = ensure_rows(c, Rp, 1))) return rc;
-  hipStream_t s = c->stream;
-  if ((rc = prep_weights(c, params))) return rc;
-  const long long n = (long long)Rp * c->Dp;
-  bool from_pf;
-  if ((rc = select_paths(c, nullptr, from_pf))) return rc;
-  RUN(c, "netu_input", 0.0, 0.0,
-      netu_input_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
-  if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
-  if ((rc = forward_and_inputgrad(c, R, Rp, true))) return rc;
-  {
-    ChainArgs a = base_args(c);
-    zgemm_args(c, a);
-    if ((rc = chain<EPI_STORE>(c, "gemm_z", a, Rp, c->Dp, c->Dp / 16, zgemm_flops(c, R), 0.0))) return rc;
-  }
-  const long long m = (long long)R * D;
-  RUN(c, "export", 0.0, 0.0,
-      export_kernel<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, nullptr, u,
-                                                                Du));
-  return DBSDE_OK;
-}
-
-int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, float* v, const dbsde_optim* o) {
-  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
-  if (!params || !grad || !o) return fail(c, DBSDE_EINVAL, "bad optimizer arguments");
+// dbsde_optim -> the kernel's OptArgs (scalar factors in double, as
+// torch.optim computes them in Python floats)
+int make_optargs(dbsde_ctx* c, const dbsde_optim* o, OptArgs& a) {
   if (o->kind < DBSDE_OPT_ADAM || o->kind > DBSDE_OPT_ASGD) return fail(c, DBSDE_EINVAL, "unknown optimizer kind");
-  const bool needs_m = o->kind == DBSDE_OPT_ADAM || o->kind == DBSDE_OPT_ADAMW || o->kind == DBSDE_OPT_ADAMAX ||
-                       o->kind == DBSDE_OPT_ADADELTA || o->kind == DBSDE_OPT_ASGD;
-  const bool needs_v = o->kind != DBSDE_OPT_SGD && o->kind != DBSDE_OPT_ASGD;
-  if ((needs_m && !m) || (needs_v && !v)) return fail(c, DBSDE_EINVAL, "optimizer state buffer is NULL");
   if (o->step < 1) return fail(c, DBSDE_EINVAL, "step must be >= 1");
-  HIPC(c, hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  const long long n = c->nparams;
-  // scalar factors in double, as torch.optim computes them in Python floats
-  OptArgs a{};
+  a = OptArgs{};
   a.kind = o->kind;
   a.lr = o->lr;
   a.beta2 = o->beta2;
@@ -1864,6 +1858,84 @@ int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, flo
     a.asgd_alpha_d = 0.75;   // torch.optim.ASGD defaults (alpha, t0)
     a.asgd_t0_d = 1e6;
   }
+  return DBSDE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int dbsde_loss_grad(dbsde_ctx* c, const float* params, const dbsde_batch* b, float* grad,
+                    const dbsde_outputs* out) {
+  return loss_grad_impl(c, params, b, grad, out, nullptr);
+}
+
+int dbsde_train_step(dbsde_ctx* c, float* params, const dbsde_batch* b, float* grad, float* m, float* v,
+                     const dbsde_optim* o, const dbsde_outputs* out) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!params || !grad || !o) return fail(c, DBSDE_EINVAL, "bad train_step arguments");
+  // the update can ride in the gradient finalize when nothing needs the whole
+  // gradient first: no clip (global norm), no NaN skip (the loss), a device
+  // step counter, and the tile finalize (wave-owned weight-gradient layouts)
+  const bool fuse = c->tnw && o->max_norm <= 0.f && !o->loss && o->step_state;
+  if (!fuse) {
+    int rc = loss_grad_impl(c, params, b, grad, out, nullptr);
+    if (rc) return rc;
+    return dbsde_optimizer_step(c, params, grad, m, v, o);
+  }
+  const bool needs_m = o->kind == DBSDE_OPT_ADAM || o->kind == DBSDE_OPT_ADAMW || o->kind == DBSDE_OPT_ADAMAX ||
+                       o->kind == DBSDE_OPT_ADADELTA || o->kind == DBSDE_OPT_ASGD;
+  const bool needs_v = o->kind != DBSDE_OPT_SGD && o->kind != DBSDE_OPT_ASGD;
+  if ((needs_m && !m) || (needs_v && !v)) return fail(c, DBSDE_EINVAL, "optimizer state buffer is NULL");
+  FusedOpt fo{};
+  int rc = make_optargs(c, o, fo.a);
+  if (rc) return rc;
+  fo.prm = params;
+  fo.m = m;
+  fo.v = v;
+  return loss_grad_impl(c, params, b, grad, out, &fo);
+}
+
+int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const float* X, float* u, float* Du) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!params || !t || !X || R < 1) return fail(c, DBSDE_EINVAL, "bad net_u arguments");
+  HIPC(c, hipSetDevice(c->device));
+  const int Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD, D = c->D;
+  int rc;
+  if ((rc = ensure_rows(c, Rp, 1))) return rc;
+  hipStream_t s = c->stream;
+  if ((rc = prep_weights(c, params))) return rc;
+  const long long n = (long long)Rp * c->Dp;
+  bool from_pf;
+  if ((rc = select_paths(c, nullptr, from_pf))) return rc;
+  RUN(c, "netu_input", 0.0, 0.0,
+      netu_input_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
+  if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
+  if ((rc = forward_and_inputgrad(c, R, Rp, true))) return rc;
+  {
+    ChainArgs a = base_args(c);
+    zgemm_args(c, a);
+    if ((rc = chain<EPI_STORE>(c, "gemm_z", a, Rp, c->Dp, c->Dp / 16, zgemm_flops(c, R), 0.0))) return rc;
+  }
+  const long long m = (long long)R * D;
+  RUN(c, "export", 0.0, 0.0,
+      export_kernel<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, nullptr, u,
+                                                                Du));
+  return DBSDE_OK;
+}
+
+int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, float* v, const dbsde_optim* o) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!params || !grad || !o) return fail(c, DBSDE_EINVAL, "bad optimizer arguments");
+  const bool needs_m = o->kind == DBSDE_OPT_ADAM || o->kind == DBSDE_OPT_ADAMW || o->kind == DBSDE_OPT_ADAMAX ||
+                       o->kind == DBSDE_OPT_ADADELTA || o->kind == DBSDE_OPT_ASGD;
+  const bool needs_v = o->kind != DBSDE_OPT_SGD && o->kind != DBSDE_OPT_ASGD;
+  if ((needs_m && !m) || (needs_v && !v)) return fail(c, DBSDE_EINVAL, "optimizer state buffer is NULL");
+  OptArgs a;
+  int rc = make_optargs(c, o, a);
+  if (rc) return rc;
+  HIPC(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const long long n = c->nparams;
   if (o->max_norm > 0.f)
     RUN(c, "grad_sqnorm", 2.0 * n, 4.0 * n, sqnorm_kernel<<<c->opt_nparts, 256, 0, s>>>(grad, c->d_used, n, c->opt_part));
   RUN(c, "optimizer", 10.0 * n, 24.0 * n,

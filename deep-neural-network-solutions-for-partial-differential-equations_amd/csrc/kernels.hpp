@@ -573,6 +573,14 @@ __global__ void __launch_bounds__(256) fill_col0_kernel(float* buf, int ld, long
 // --------------------------------------------------------------------------
 enum PackMode { PK_COPY = 0, PK_ADD2 = 1, PK_NEGPROJ = 2, PK_SLABSUM = 3 };
 constexpr int NAIS_LMAX = 128;   // NAIS projection matrices: L x L, L <= 128 (rtr / proj kernels)
+// |R|_F from the rtr partials (at most 64, one per lane) in a fixed order: a
+// xor butterfly, the order pack_tagged_kernel's norm also follows
+__device__ __forceinline__ double nais_norm_from(double part_of_lane) {
+  double sq = part_of_lane;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+  return sqrt(sq);
+}
 struct PackDesc {
   const float* src;
   const float* src2;   // PK_ADD2 second source
@@ -678,6 +686,70 @@ __device__ inline void opt_step_scalars(OptArgs& a, double t) {
   }
 }
 
+// one parameter element of the update: params / moments at index i, its
+// (clipped) gradient gi
+__device__ __forceinline__ void opt_update(const OptArgs& a, long long i, float gi, float* prm, float* m, float* v) {
+  float p = prm[i];
+  switch (a.kind) {
+    case OPT_SGD: {
+      if (a.wd != 0.f) gi = gi + a.wd * p;
+      prm[i] = p - a.lr * gi;
+      break;
+    }
+    case OPT_RMSPROP: {   // square_avg.mul_(alpha).addcmul_(g, g, 1-alpha); p.addcdiv_(g, sqrt(sa)+eps, -lr)
+      if (a.wd != 0.f) gi = gi + a.wd * p;
+      const float sa = v[i] * a.alpha + a.omb2 * gi * gi;
+      v[i] = sa;
+      prm[i] = p + (-a.lr) * (gi / (sqrtf(sa) + a.eps));
+      break;
+    }
+    case OPT_ADAGRAD: {   // state_sum.addcmul_(g, g, 1); p.addcdiv_(g, sqrt(ss)+eps, -clr)
+      if (a.wd != 0.f) gi = gi + a.wd * p;
+      const float ss = v[i] + gi * gi;
+      v[i] = ss;
+      prm[i] = p + (-a.step_size) * (gi / (sqrtf(ss) + a.eps));
+      break;
+    }
+    case OPT_ADAMAX: {    // exp_avg.lerp_(g, 1-b1); exp_inf = max(exp_inf*b2, |g|+eps); p.addcdiv_(m, u, -clr)
+      if (a.wd != 0.f) gi = gi + a.wd * p;
+      const float mi = m[i] + a.omb1 * (gi - m[i]);
+      const float ui = fmaxf(v[i] * a.beta2, fabsf(gi) + a.eps);
+      m[i] = mi;
+      v[i] = ui;
+      prm[i] = p + (-a.step_size) * (mi / ui);
+      break;
+    }
+    case OPT_ADADELTA: {  // sq.mul_(rho).addcmul_(g,g,1-rho); d = sqrt(acc+eps)/sqrt(sq+eps)*g; acc.mul_(rho).addcmul_(d,d,1-rho)
+      if (a.wd != 0.f) gi = gi + a.wd * p;
+      const float sq = v[i] * a.rho + a.omb2 * gi * gi;
+      const float dl = sqrtf(m[i] + a.eps) / sqrtf(sq + a.eps) * gi;
+      v[i] = sq;
+      m[i] = m[i] * a.rho + a.omb2 * dl * dl;
+      prm[i] = p + (-a.lr) * dl;
+      break;
+    }
+    case OPT_ASGD: {      // p.mul_(1 - lambd eta); p.add_(g, -eta); ax = p (mu == 1) or ax += (p - ax) mu
+      if (a.wd != 0.f) gi = gi + a.wd * p;
+      p = p * a.asgd_decay;
+      p = p + (-a.asgd_eta) * gi;
+      prm[i] = p;
+      m[i] = a.asgd_copy ? p : m[i] + (p - m[i]) * a.asgd_mu;
+      break;
+    }
+    default: {            // Adam / AdamW
+      if (a.kind == OPT_ADAMW) p = p * (1.f - a.lr * a.wd);   // decoupled decay
+      else if (a.wd != 0.f) gi = gi + a.wd * p;                // Adam L2
+      float mi = m[i];
+      mi = mi + a.omb1 * (gi - mi);                            // exp_avg.lerp_(g, 1-beta1)
+      float vi = v[i] * a.beta2 + a.omb2 * gi * gi;            // mul_(beta2).addcmul_(g, g, 1-beta2)
+      m[i] = mi;
+      v[i] = vi;
+      const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
+      prm[i] = p - a.step_size * (mi / denom);                 // addcdiv_(m, denom, -step_size)
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float* m, float* v, const unsigned char* used,
                                                     long long n, const double* part, OptArgs a) {
   __shared__ float clip_s;
@@ -709,68 +781,31 @@ __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float*
   const float coef = clip_s;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     if (!used[i]) continue;
-    float gi = g[i] * coef;
+    const float gi = g[i] * coef;
     g[i] = gi;
-    float p = prm[i];
-    switch (a.kind) {
-      case OPT_SGD: {
-        if (a.wd != 0.f) gi = gi + a.wd * p;
-        prm[i] = p - a.lr * gi;
-        break;
-      }
-      case OPT_RMSPROP: {   // square_avg.mul_(alpha).addcmul_(g, g, 1-alpha); p.addcdiv_(g, sqrt(sa)+eps, -lr)
-        if (a.wd != 0.f) gi = gi + a.wd * p;
-        const float sa = v[i] * a.alpha + a.omb2 * gi * gi;
-        v[i] = sa;
-        prm[i] = p + (-a.lr) * (gi / (sqrtf(sa) + a.eps));
-        break;
-      }
-      case OPT_ADAGRAD: {   // state_sum.addcmul_(g, g, 1); p.addcdiv_(g, sqrt(ss)+eps, -clr)
-        if (a.wd != 0.f) gi = gi + a.wd * p;
-        const float ss = v[i] + gi * gi;
-        v[i] = ss;
-        prm[i] = p + (-a.step_size) * (gi / (sqrtf(ss) + a.eps));
-        break;
-      }
-      case OPT_ADAMAX: {    // exp_avg.lerp_(g, 1-b1); exp_inf = max(exp_inf*b2, |g|+eps); p.addcdiv_(m, u, -clr)
-        if (a.wd != 0.f) gi = gi + a.wd * p;
-        const float mi = m[i] + a.omb1 * (gi - m[i]);
-        const float ui = fmaxf(v[i] * a.beta2, fabsf(gi) + a.eps);
-        m[i] = mi;
-        v[i] = ui;
-        prm[i] = p + (-a.step_size) * (mi / ui);
-        break;
-      }
-      case OPT_ADADELTA: {  // sq.mul_(rho).addcmul_(g,g,1-rho); d = sqrt(acc+eps)/sqrt(sq+eps)*g; acc.mul_(rho).addcmul_(d,d,1-rho)
-        if (a.wd != 0.f) gi = gi + a.wd * p;
-        const float sq = v[i] * a.rho + a.omb2 * gi * gi;
-        const float dl = sqrtf(m[i] + a.eps) / sqrtf(sq + a.eps) * gi;
-        v[i] = sq;
-        m[i] = m[i] * a.rho + a.omb2 * dl * dl;
-        prm[i] = p + (-a.lr) * dl;
-        break;
-      }
-      case OPT_ASGD: {      // p.mul_(1 - lambd eta); p.add_(g, -eta); ax = p (mu == 1) or ax += (p - ax) mu
-        if (a.wd != 0.f) gi = gi + a.wd * p;
-        p = p * a.asgd_decay;
-        p = p + (-a.asgd_eta) * gi;
-        prm[i] = p;
-        m[i] = a.asgd_copy ? p : m[i] + (p - m[i]) * a.asgd_mu;
-        break;
-      }
-      default: {            // Adam / AdamW
-        if (a.kind == OPT_ADAMW) p = p * (1.f - a.lr * a.wd);   // decoupled decay
-        else if (a.wd != 0.f) gi = gi + a.wd * p;                // Adam L2
-        float mi = m[i];
-        mi = mi + a.omb1 * (gi - mi);                            // exp_avg.lerp_(g, 1-beta1)
-        float vi = v[i] * a.beta2 + a.omb2 * gi * gi;            // mul_(beta2).addcmul_(g, g, 1-beta2)
-        m[i] = mi;
-        v[i] = vi;
-        const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
-        prm[i] = p - a.step_size * (mi / denom);                 // addcdiv_(m, denom, -step_size)
-      }
-    }
+    opt_update(a, i, gi, prm, m, v);
   }
+}
+
+// The optimizer folded into the gradient finalize (single process, no clip,
+// no NaN skip, device step counter): every finalize thread that writes the
+// gradient of a parameter element also applies the update to it, so the
+// step needs no separate optimizer launch.  step_writer: the one block that
+// advances the counter.
+struct FusedOpt {
+  float *prm, *m, *v;
+  OptArgs a;   // a.state set (device step count)
+};
+__device__ __forceinline__ void fused_opt_prologue(FusedOpt& fo, bool step_writer) {
+  __shared__ OptArgs fa_s;
+  if (threadIdx.x == 0) {
+    const double done = fo.a.state[fo.a.parity];
+    opt_step_scalars(fo.a, done + 1.0);
+    if (step_writer) fo.a.state[1 - fo.a.parity] = done + 1.0;
+    fa_s = fo.a;
+  }
+  __syncthreads();
+  fo.a = fa_s;
 }
 
 // --------------------------------------------------------------------------
@@ -863,8 +898,9 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
 constexpr int TF_ELEMS = 256;   // elements per block (64 lanes x float4)
 __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int ndesc, const float* slab, int S,
                                                       int P, int T, float* grad, const double* loss_part, int nloss,
-                                                      float* loss) {
+                                                      float* loss, FusedOpt fo, int fuse) {
   const int p = blockIdx.y;
+  if (fuse) fused_opt_prologue(fo, p == P && blockIdx.x == 0);
   if (p == P) {   // zero windows (NAIS-Net's never-used input_layers[K])
     // and, in block 0, the loss sum (loss_final_kernel's fixed order: one
     // launch fewer on the step's critical path)
@@ -938,11 +974,11 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
         if (rr < 0 || rr >= d.rows || ck < 0 || ck >= d.cols) continue;
         const float fv = d.scale * (float)v;
         uintptr_t dv = (uintptr_t)d.dst;
-        float* dst = (dv & ((uintptr_t)1 << 61)) ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
-        if (d.transpose)
-          dst[(size_t)ck * d.dst_ld + rr] = fv;
-        else
-          dst[(size_t)rr * d.dst_ld + ck] = fv;
+        const bool to_grad = dv & ((uintptr_t)1 << 61);
+        float* dst = to_grad ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
+        const size_t off = d.transpose ? (size_t)ck * d.dst_ld + rr : (size_t)rr * d.dst_ld + ck;
+        dst[off] = fv;
+        if (fuse && to_grad) opt_update(fo.a, (dst - grad) + (long long)off, fv, fo.prm, fo.m, fo.v);
         if (d.dotR) dp += (double)fv * (double)d.dotR[(size_t)rr * d.dst_ld + ck];
       }
     }

@@ -277,8 +277,9 @@ class FBSNN(ABC):
                 "v": torch.zeros_like(self.params), "dstep": torch.zeros(2, dtype=torch.float64, device=self.device),
                 "calls": 0}
 
-    def _update(self, opt, learning_rate=None, skip_loss=None):
-        """clip_grad_norm_ (not for LBFGS) + optimizer.step() on the device."""
+    def _opt_kwargs(self, opt, learning_rate=None, skip_loss=None):
+        """The optimizer_step keywords of the next update of `opt` (advances its
+        launch count: the device step counter's ping-pong slot)."""
         kind = opt["kind"]
         if kind == "LBFGS":
             raise ValueError("LBFGS steps need a closure (FBSNN._lbfgs_step)")
@@ -286,12 +287,16 @@ class FBSNN(ABC):
         kw = OPT_DEFAULTS[kind]
         parity = opt["calls"] & 1
         opt["calls"] += 1
-        self.solver.optimizer_step(
-            self.params, self.grad, opt["m"], opt["v"], kind=kind, lr=lr, betas=kw.get("betas", (0.9, 0.999)),
-            eps=kw.get("eps", 1e-8), weight_decay=kw["weight_decay"], max_norm=self.clip_max_norm or 0.0,
-            step=opt["calls"], alpha=kw.get("alpha", 0.99) if kind == "RMSprop" else 0.99, rho=kw.get("rho", 0.9),
-            lr_decay=kw.get("lr_decay", 0.0), lambd=kw.get("lambd", 1e-4), skip_nonfinite_loss=skip_loss,
-            step_state=opt["dstep"], step_parity=parity)
+        return dict(kind=kind, lr=lr, betas=kw.get("betas", (0.9, 0.999)), eps=kw.get("eps", 1e-8),
+                    weight_decay=kw["weight_decay"], max_norm=self.clip_max_norm or 0.0, step=opt["calls"],
+                    alpha=kw.get("alpha", 0.99) if kind == "RMSprop" else 0.99, rho=kw.get("rho", 0.9),
+                    lr_decay=kw.get("lr_decay", 0.0), lambd=kw.get("lambd", 1e-4), skip_nonfinite_loss=skip_loss,
+                    step_state=opt["dstep"], step_parity=parity)
+
+    def _update(self, opt, learning_rate=None, skip_loss=None):
+        """clip_grad_norm_ (not for LBFGS) + optimizer.step() on the device."""
+        self.solver.optimizer_step(self.params, self.grad, opt["m"], opt["v"],
+                                   **self._opt_kwargs(opt, learning_rate, skip_loss))
 
     def optimizer_steps_taken(self, opt):
         """Updates the device has applied (skipped ones excluded); syncs."""
@@ -442,6 +447,14 @@ class FBSNN(ABC):
         lbfgs = opt_state["kind"] == "LBFGS"
         if next_seed is not None and not lbfgs:
             self.solver.prefetch(ml, self.N, xi, seed=next_seed, path0=p0)
+        if self.world == 1 and not lbfgs:
+            # one process: loss, gradient and update in one native call (the
+            # update folds into the gradient finalize when it can)
+            self.solver.train_step(self.params, ml, self.N, xi, self.grad, opt_state["m"], opt_state["v"],
+                                   self._opt_kwargs(opt_state, learning_rate,
+                                                    self._gradbuf[-1:] if self.skip_nonfinite else None),
+                                   seed=seed, path0=p0, loss=self._gradbuf[-1:])
+            return self._gradbuf[-1:]
         self.solver.loss_grad(self.params, ml, self.N, xi, seed=seed, path0=p0,
                               grad=self.grad, loss=self._gradbuf[-1:])
         loss = self._reduce()

@@ -117,9 +117,7 @@ class NativeSolver:
         s = torch.cuda.current_stream(self.device).cuda_stream
         _lib.check(self.lib.dbsde_set_stream(self.ctx, ctypes.c_void_p(s)), self.ctx)
 
-    def loss_grad(self, params, M, N, Xi, t=None, W=None, seed=0, offset=0, path0=0, grad=None, loss=None,
-                  X=None, Y=None, Z=None):
-        """FBSNN.loss_function (+ loss.backward when grad is given)."""
+    def _batch_out(self, params, M, N, Xi, t, W, seed, offset, path0, grad, loss, X, Y, Z):
         D = self.D
         self._check_tensor(params, "params", self.nparams)
         self._check_tensor(grad, "grad", self.nparams)
@@ -134,10 +132,27 @@ class NativeSolver:
         self._check_tensor(Z, "Z", M * (N + 1) * D)
         b = _lib.Batch(int(M), int(N), _ptr(t), _ptr(W), int(seed) & (2 ** 64 - 1),
                        int(offset) & (2 ** 64 - 1), int(path0), _ptr(Xi), Xi.numel() // D)
-        o = _lib.Outputs(_ptr(loss), _ptr(X), _ptr(Y), _ptr(Z))
+        return b, _lib.Outputs(_ptr(loss), _ptr(X), _ptr(Y), _ptr(Z))
+
+    def loss_grad(self, params, M, N, Xi, t=None, W=None, seed=0, offset=0, path0=0, grad=None, loss=None,
+                  X=None, Y=None, Z=None):
+        """FBSNN.loss_function (+ loss.backward when grad is given)."""
+        b, o = self._batch_out(params, M, N, Xi, t, W, seed, offset, path0, grad, loss, X, Y, Z)
         self._bind_stream()
         _lib.check(self.lib.dbsde_loss_grad(self.ctx, _ptr(params), ctypes.byref(b), _ptr(grad),
                                             ctypes.byref(o)), self.ctx)
+
+    def train_step(self, params, M, N, Xi, grad, m, v, opt, t=None, W=None, seed=0, offset=0, path0=0, loss=None,
+                   X=None, Y=None, Z=None):
+        """loss_grad + optimizer_step of one process (dbsde_train_step: the
+        update is folded into the gradient finalize when it needs no clip, no
+        NaN skip and has a device step counter).  opt: the keyword arguments
+        of optimizer_step."""
+        b, o = self._batch_out(params, M, N, Xi, t, W, seed, offset, path0, grad, loss, X, Y, Z)
+        op = self._optim(params, grad, m, v, **opt)
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_train_step(self.ctx, _ptr(params), ctypes.byref(b), _ptr(grad), _ptr(m), _ptr(v),
+                                             ctypes.byref(op), ctypes.byref(o)), self.ctx)
 
     def prefetch(self, M, N, Xi, seed=0, offset=0, path0=0):
         """Roll out the device-mode batch a later loss_grad(M, N, Xi, seed=...,
@@ -167,14 +182,22 @@ class NativeSolver:
         _lib.check(self.lib.dbsde_net_u(self.ctx, _ptr(params), R, _ptr(t), _ptr(X), _ptr(u), _ptr(Du)),
                    self.ctx)
 
-    def optimizer_step(self, params, grad, m, v, kind="Adam", lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                       weight_decay=0.0, max_norm=0.0, step=1, alpha=0.99, rho=0.9, lr_decay=0.0, lambd=1e-4,
-                       asgd_eta=0.0, asgd_mu=1.0, skip_nonfinite_loss=None, step_state=None, step_parity=0):
+    def optimizer_step(self, params, grad, m, v, **opt):
         """clip_grad_norm_ + optimizer.step() over the flat parameters; m, v are
-        the optimizer's state buffers (see include/dbsde.h DBSDE_OPT_*).
-        step_state: optional device float64[2] step counter (dbsde_optim.step_state):
-        the update number, and from it the step-dependent scalars, then come from
-        the device, and a skipped update does not advance it."""
+        the optimizer's state buffers (see include/dbsde.h DBSDE_OPT_*); opt as
+        _optim."""
+        o = self._optim(params, grad, m, v, **opt)
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_optimizer_step(self.ctx, _ptr(params), _ptr(grad), _ptr(m), _ptr(v),
+                                                 ctypes.byref(o)), self.ctx)
+
+    def _optim(self, params, grad, m, v, kind="Adam", lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+               weight_decay=0.0, max_norm=0.0, step=1, alpha=0.99, rho=0.9, lr_decay=0.0, lambd=1e-4,
+               asgd_eta=0.0, asgd_mu=1.0, skip_nonfinite_loss=None, step_state=None, step_parity=0):
+        """The dbsde_optim block.  step_state: optional device float64[2] step
+        counter (dbsde_optim.step_state): the update number, and from it the
+        step-dependent scalars, then come from the device, and a skipped update
+        does not advance it."""
         if kind not in _lib.OPTIMIZERS:
             raise ValueError(f"Optimizer type '{kind}' is not recognized.")
         for name, v_ in (("params", params), ("grad", grad), ("m", m), ("v", v)):
@@ -183,12 +206,9 @@ class NativeSolver:
         if step_state is not None and (step_state.device != self.device or step_state.dtype != torch.float64
                                        or step_state.numel() != 2):
             raise ValueError(f"step_state must be a float64 tensor of 2 elements on {self.device}")
-        o = _lib.Optim(_lib.OPTIMIZERS[kind], lr, betas[0], betas[1], eps, weight_decay,
-                       max_norm if max_norm else 0.0, int(step), alpha, rho, lr_decay, lambd, asgd_eta, asgd_mu,
-                       _ptr(skip_nonfinite_loss), _ptr(step_state), int(step_parity))
-        self._bind_stream()
-        _lib.check(self.lib.dbsde_optimizer_step(self.ctx, _ptr(params), _ptr(grad), _ptr(m), _ptr(v),
-                                                 ctypes.byref(o)), self.ctx)
+        return _lib.Optim(_lib.OPTIMIZERS[kind], lr, betas[0], betas[1], eps, weight_decay,
+                          max_norm if max_norm else 0.0, int(step), alpha, rho, lr_decay, lambd, asgd_eta, asgd_mu,
+                          _ptr(skip_nonfinite_loss), _ptr(step_state), int(step_parity))
 
     # ------------------------------------------------------------------ L-BFGS vector primitives
     def vec_reduce(self, op, a, b=None):

@@ -255,6 +255,20 @@ int dbsde_optimizer_step(dbsde_ctx* ctx, float* params, float* grad, float* m, f
                          const dbsde_optim* opt);
 
 /*
+ * One training iteration of one process: dbsde_loss_grad followed by
+ * dbsde_optimizer_step (nd_BSPDE_case.py:376-384: loss.backward(),
+ * clip_grad_norm_, optimizer.step()).  When the update needs nothing but each
+ * element's own gradient -- no clipping (max_norm <= 0), no NaN skip (loss ==
+ * NULL) and a device step counter (step_state) -- it is applied inside the
+ * gradient finalize kernels, element by element as each gradient is formed
+ * (one launch fewer per step; grad is still written).  Otherwise the two calls
+ * run in sequence.  Data-parallel callers, whose all-reduce sits between the
+ * gradient and the update, use the two calls instead.
+ */
+int dbsde_train_step(dbsde_ctx* ctx, float* params, const dbsde_batch* batch, float* grad, float* m, float* v,
+                     const dbsde_optim* opt, const dbsde_outputs* out);
+
+/*
  * L-BFGS (torch.optim.LBFGS(params, lr) as nd_BSPDE_case.py:347-348 and
  * with_corr...py:386-387 build it; train() calls optimizer.step(closure) with a
  * closure that re-runs loss_function + backward on the same batch, without

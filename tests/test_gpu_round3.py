@@ -141,12 +141,9 @@ def test_config5_fused_and_per_layer_paths_agree(pkg, dev):
 def _basket_case(pkg, dev, M):
     D, N = 100, 50
     layers = [D + 1] + 4 * [110] + [1]
+    np.random.seed(3)
+    L = np.linalg.cholesky(pkg.FBSNN._random_corr(D, False))      # the Q10 recipe (with_corr...py:187-212)
     rs = np.random.RandomState(3)
-    a = rs.normal(size=(D, D))
-    c = a @ a.T
-    np.fill_diagonal(c, 1)
-    d = np.sqrt(np.diag(c))
-    L = np.linalg.cholesky(c / np.outer(d, d) + 1e-6 * np.eye(D))
     dw = np.einsum("ij,mnj->mni", L, np.sqrt(1.0 / N) * rs.normal(size=(M, N, D)))
     W = np.concatenate([np.zeros((M, 1, D)), np.cumsum(dw, 1)], 1).astype(np.float32)
     t = np.tile(np.concatenate([[0.0], np.cumsum(np.full(N, 1.0 / N))]), (M, 1)).astype(np.float32)
@@ -339,3 +336,29 @@ def test_device_step_sees_an_in_place_xi_change(pkg, dev):
     twin.Xi.mul_(1.5)
     l_twin = float(twin.device_step(topt, seed=2))
     assert l_changed == l_twin
+
+
+@pytest.mark.parametrize("name", ["Adam", "RMSprop", "ASGD"])
+def test_fused_update_equals_separate_optimizer(pkg, dev, name):
+    """dbsde_train_step folds the update into the gradient finalize (one
+    process, no clip): three device steps give bit-identical parameters,
+    moments and step count to dbsde_loss_grad + dbsde_optimizer_step."""
+    g = _load("g2_north_star.npz")
+    layers = [int(v) for v in g["layers"]]
+    D = layers[0] - 1
+
+    def model():
+        m = pkg.BlackScholesBarenblatt(g["Xi"], 1.0, 256, 10, D, layers, "NAIS-Net", "Sine", device=dev)
+        m.params.copy_(torch.from_numpy(g["params"]).to(dev))
+        return m
+
+    a, b = model(), model()
+    oa, ob = a.new_optimizer_state(name, 1e-3), b.new_optimizer_state(name, 1e-3)
+    for s in range(3):
+        a.device_step(oa, seed=s)                                          # fused
+        b.solver.loss_grad(b.params, b.M, b.N, b._device_xi(0, b.M), seed=s, grad=b.grad, loss=b._gradbuf[-1:])
+        b._update(ob)                                                      # separate launches
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
+    assert torch.equal(oa["m"], ob["m"]) and torch.equal(oa["v"], ob["v"])
+    assert a.optimizer_steps_taken(oa) == b.optimizer_steps_taken(ob) == 3
