@@ -929,6 +929,17 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int TT = T * T;
   const int e0 = blockIdx.x * TF_ELEMS + 4 * lane;   // T % 4 == 0: the float4 stays in one row
+  // this problem's windows, compacted into LDS once per block (the scatter
+  // below then walks 2-5 windows, not every descriptor)
+  constexpr int TF_WMAX = 16;
+  __shared__ PackDesc wins[TF_WMAX];
+  __shared__ int nwin_s;
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int i = 0; i < ndesc && n < TF_WMAX; ++i)
+      if (descs[i].nslab != 0 && descs[i].sp == p) wins[n++] = descs[i];
+    nwin_s = n;
+  }
   const long long stride = (long long)P * TT;
   double s4[4] = {0.0, 0.0, 0.0, 0.0};
   if (e0 < TT) {
@@ -961,15 +972,15 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
   if (grp != 0) return;
   double dp = 0.0;
   const PackDesc* dotd = nullptr;
+  const int nwin = nwin_s;
   if (e0 < TT) {
     const int r = e0 / T, c00 = e0 - r * T;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const double v = (part[0][c][lane] + part[1][c][lane]) + (part[2][c][lane] + part[3][c][lane]);
       const int cc = c00 + c;
-      for (int i = 0; i < ndesc; ++i) {
-        const PackDesc& d = descs[i];
-        if (d.nslab == 0 || d.sp != p) continue;
+      for (int i = 0; i < nwin; ++i) {
+        const PackDesc& d = wins[i];
         const int rr = r - d.sr0, ck = cc - d.sc0;
         if (rr < 0 || rr >= d.rows || ck < 0 || ck >= d.cols) continue;
         const float fv = d.scale * (float)v;
@@ -983,8 +994,8 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
       }
     }
   }
-  for (int i = 0; i < ndesc; ++i)
-    if (descs[i].nslab != 0 && descs[i].sp == p && descs[i].dotR) dotd = &descs[i];
+  for (int i = 0; i < nwin; ++i)
+    if (wins[i].dotR) dotd = &wins[i];
   if (dotd) {   // fixed-order wave reduction of the block's <Abar, R> partial
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
