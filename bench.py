@@ -42,7 +42,8 @@ PEAK_FP32_MFMA_TFLOPS = 157.3                                # MI355X_MICROARCH.
 # bf16 MFMAs, so their fp32-equivalent matrix peak is the dense bf16 peak / 6
 PEAK_BF16_DENSE_TFLOPS = 2500.0
 PEAK_X3_TFLOPS = PEAK_BF16_DENSE_TFLOPS / 6.0
-X3_RECORDS = {1: ("fused_phases_pipelined", "fused_fwd_inputgrad", "fused_tangent_reverse"), 2: ("tn_weight_grad",)}
+X3_RECORDS = {1: ("fused_phases_pipelined", "fused_fwd_inputgrad", "fused_tangent_reverse"), 2: ("tn_weight_grad",),
+              4: ("gemm_",)}
 PEAK_HBM_GBS = 8000.0
 PROFILE_ROUND = "r2"          # profiles/<round>_pmc_* counter collections of the current build
 # rocprof symbol of each profiled launch class (EPI ids from csrc/kernels.hpp)

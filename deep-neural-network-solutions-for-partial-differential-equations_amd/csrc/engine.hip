@@ -25,6 +25,7 @@
 #include "kernels.hpp"
 #include "paths.hpp"
 #include "phase.hpp"
+#include "chainx3.hpp"
 #include "tnw.hpp"
 #include "vec.hpp"
 
@@ -155,6 +156,7 @@ struct dbsde_ctx {
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
   bool x3 = false;                // ... in their split-bf16 form (phase.hpp)
+  bool x3chain = false;           // per-layer chain GEMMs in split-bf16 form (chainx3.hpp)
   // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
   // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
   std::vector<float*> imgX, imgZ, imgF, imgB;
@@ -400,6 +402,10 @@ int build_net(dbsde_ctx* c) {
   c->x3 = want_x3 && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, true) >= 0;
   c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3) >= 0;
   c->x3 = c->x3 && c->fused;
+  // FC / Resnet layouts the fused kernels do not cover: split-bf16 chain GEMMs
+  // (uniform hidden width, output blocks a multiple of the column tile)
+  c->x3chain = want_x3 && !c->fused && !c->has_v && uniform && c->Dp <= 128;
+  for (int j = 0; j <= c->K && c->x3chain; ++j) c->x3chain = (c->Wp[j] / 16) % nt_for(c->Wp[j]) == 0;
   // problem kind: Brownian dimension, g columns, u clamp
   const dbsde_problem& pr = g.problem;
   if (pr.kind != DBSDE_PROB_DIAG && pr.kind != DBSDE_PROB_HESTON) return fail(c, DBSDE_EINVAL, "unknown problem kind");
@@ -491,10 +497,11 @@ int build_buffers(dbsde_ctx* c) {
   c->imgB.assign(K + 1, nullptr);
   // floats of an image with tout output / tin input blocks of 16: fp32
   // fragments (1 KiB each), or split-bf16 fragments (3 KiB per 32-wide block)
+  const bool img_x3 = c->x3 || c->x3chain;
   auto img_floats = [&](int tout, int tin) -> size_t {
-    return c->x3 ? (size_t)tout * ((tin + 1) / 2) * 768 : (size_t)tout * tin * 256;
+    return img_x3 ? (size_t)tout * ((tin + 1) / 2) * 768 : (size_t)tout * tin * 256;
   };
-  if (c->fused) {
+  if (c->fused || c->x3chain) {
     for (int j = 0; j <= (c->has_v ? K : 0); ++j) {
       if ((rc = dalloc_t(c, &c->imgX[j], img_floats(TW, TDp)))) return rc;
       if ((rc = dalloc_t(c, &c->imgZ[j], img_floats(TDp, TW)))) return rc;
@@ -504,7 +511,7 @@ int build_buffers(dbsde_ctx* c) {
       if ((rc = dalloc_t(c, &c->imgB[j], img_floats(TW, TW)))) return rc;
     }
   }
-  const int fsplit = c->x3 ? 1 : 0;
+  const int fsplit = img_x3 ? 1 : 0;
   auto frag = [fsplit](PackDesc d, float* img, int tin, int tout, int row0, int col0) {
     d.fdst = img;
     d.ftin = tin;
@@ -742,6 +749,19 @@ int chain(dbsde_ctx* c, const char* name, ChainArgs& a, int Rp, int NP, int NT, 
   if (NP % (16 * NT) != 0) return fail(c, DBSDE_EINVAL, "internal: column tiling mismatch");
   if (a.K % CH_KC != 0) return fail(c, DBSDE_EINVAL, "internal: K not a multiple of 16");
   hipStream_t s = c->stream;
+  if (a.x3_img) {   // split-bf16 form: the weight image must hold this launch's output columns
+    if (a.x3_tout < NP / 16 || a.x3_ti * 16 < a.K) return fail(c, DBSDE_EINVAL, "internal: x3 chain image geometry");
+    switch (NT) {
+      case 7:
+        RUN(c, name, flops, bytes, (chain_gemm_kernel<7, EPI, true><<<grid, 256, 0, s>>>(a)));
+        return DBSDE_OK;
+      case 8:
+        RUN(c, name, flops, bytes, (chain_gemm_kernel<8, EPI, true><<<grid, 256, 0, s>>>(a)));
+        return DBSDE_OK;
+      default:
+        return fail(c, DBSDE_EINVAL, "internal: x3 chain tile");
+    }
+  }
 #define CASE_NT(X) \
   case X:          \
     RUN(c, name, flops, bytes, chain_gemm_kernel<X, EPI><<<grid, 256, 0, s>>>(a)); \
@@ -768,6 +788,14 @@ ChainArgs base_args(dbsde_ctx* c) {
   a.rho = c->rho;
   a.act = c->act;
   return a;
+}
+// the split-bf16 chain form of a launch: weight image img with tout output /
+// ti input 16-blocks (no-op for the fp32 chain)
+void x3_weights(dbsde_ctx* c, ChainArgs& a, const float* img, int tout, int ti) {
+  if (!c->x3chain) return;
+  a.x3_img = (const unsigned short*)img;
+  a.x3_tout = tout;
+  a.x3_ti = ti;
 }
 
 constexpr int ROW_PAD = P3_ROWS;   // rows per phase-kernel workgroup (a multiple of the chain-GEMM tile, 64)
@@ -1172,6 +1200,7 @@ int forward_and_inputgrad(dbsde_ctx* c, int R, int Rp, bool need_u_only_and_z_st
     a.A = c->xin;
     a.lda = c->Dp;
     a.Bt = c->BtIn;
+    x3_weights(c, a, c->imgX[0], c->Wp[0] / 16, c->Dp / 16);
     a.ldb = c->Dp;
     a.K = c->Dp;
     a.out[0] = c->Abuf;
@@ -1191,6 +1220,7 @@ int forward_and_inputgrad(dbsde_ctx* c, int R, int Rp, bool need_u_only_and_z_st
     a.A = c->H + c->col[j - 1];
     a.lda = S;
     a.Bt = c->Bf[j];
+    x3_weights(c, a, c->imgF[j], c->Wp[j] / 16, c->Wp[j - 1] / 16);
     a.ldb = c->Wp[j - 1];
     a.K = c->Wp[j - 1];
     a.in[0] = c->has_v ? c->Abuf + c->col[j] : nullptr;
@@ -1219,6 +1249,7 @@ int forward_and_inputgrad(dbsde_ctx* c, int R, int Rp, bool need_u_only_and_z_st
     a.A = c->Delta + c->col[j];
     a.lda = S;
     a.Bt = c->Bb[j];
+    x3_weights(c, a, c->imgB[j], c->Wp[j - 1] / 16, c->Wp[j] / 16);
     a.ldb = c->Wp[j];
     a.K = c->Wp[j];
     a.in[0] = j == K ? nullptr : c->G + c->col[j];
@@ -1242,6 +1273,7 @@ int zgemm_args(dbsde_ctx* c, ChainArgs& a) {
   a.A = c->Delta;
   a.lda = c->Stot;
   a.Bt = c->BtZ;
+  x3_weights(c, a, c->imgZ[0], c->Dp / 16, c->Wp[0] / 16);
   a.ldb = c->Stot_x;
   a.K = c->Stot_x;
   a.out[0] = c->zfull;
@@ -1387,7 +1419,7 @@ int dbsde_abi_version(void) { return DBSDE_ABI_VERSION; }
 
 int dbsde_matrix_form(const dbsde_ctx* c) {
   if (!c) return 0;
-  return (c->x3 ? 1 : 0) | (c->tnw && c->tnw_x3 ? 2 : 0);
+  return (c->x3 ? 1 : 0) | (c->tnw && c->tnw_x3 ? 2 : 0) | (c->x3chain ? 4 : 0);
 }
 
 const char* dbsde_last_error(const dbsde_ctx* ctx) {
@@ -1643,6 +1675,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         a.A = c->zbar;
         a.lda = c->Dp;
         a.Bt = c->BtIn;
+        x3_weights(c, a, c->imgX[0], c->Wp[0] / 16, c->Dp / 16);
         a.ldb = c->Dp;
         a.K = c->Dp;
         a.in[0] = c->Abuf;
@@ -1663,6 +1696,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         a.A = c->Hdot + c->col[j - 1];
         a.lda = S;
         a.Bt = c->Bf[j];
+        x3_weights(c, a, c->imgF[j], c->Wp[j] / 16, c->Wp[j - 1] / 16);
         a.ldb = c->Wp[j - 1];
         a.K = c->Wp[j - 1];
         a.in[0] = c->has_v ? c->Adot + c->col[j] : nullptr;
@@ -1690,6 +1724,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         a.A = c->Alpha + c->col[j];
         a.lda = S;
         a.Bt = c->Bb[j];
+        x3_weights(c, a, c->imgB[j], c->Wp[j - 1] / 16, c->Wp[j] / 16);
         a.ldb = c->Wp[j];
         a.K = c->Wp[j];
         a.in[0] = j == K ? nullptr : c->Pbuf[(j + 1) & 1];

@@ -162,6 +162,10 @@ struct ChainArgs {
   float* zbar;        // [Rp, ldx]
   float* rres;        // [Rp]
   float* lossrow;     // [Rp]
+  // split-bf16 form (chainx3.hpp): the weight as a fragment image (x3_off)
+  // with x3_tout output blocks per input block row, x3_ti 16-wide input blocks
+  const unsigned short* x3_img;
+  int x3_tout, x3_ti;
 };
 
 constexpr int CH_BM = 64;
@@ -233,12 +237,19 @@ __device__ __forceinline__ float red16(float v) {
   return v;
 }
 
-template <int NT, int EPI>
+// split-bf16 mainloop (chainx3.hpp)
+template <int NT>
+__device__ __forceinline__ void chain_x3_mainloop(const ChainArgs& p, int row0, int col0, floatx4 (&acc)[NT]);
+
+template <int NT, int EPI, bool X3 = false>
 __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
   const int row0 = blockIdx.x * CH_BM;
   const int col0 = blockIdx.y * 16 * NT;
   floatx4 acc[NT];
-  chain_mainloop<NT>(p, row0, col0, acc);
+  if constexpr (X3)
+    chain_x3_mainloop<NT>(p, row0, col0, acc);
+  else
+    chain_mainloop<NT>(p, row0, col0, acc);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rbase = row0 + wave * 16 + (lane >> 4) * 4;
