@@ -700,6 +700,9 @@ __device__ inline void opt_step_scalars(OptArgs& a, double t) {
 // one parameter element of the update: params / moments at index i, its
 // (clipped) gradient gi
 __device__ __forceinline__ void opt_update(const OptArgs& a, long long i, float gi, float* prm, float* m, float* v) {
+  // every product and sum rounded as written (torch's op-by-op formulas), and
+  // the same in every kernel that inlines this (optim_kernel, the finalize)
+#pragma clang fp contract(off)
   float p = prm[i];
   switch (a.kind) {
     case OPT_SGD: {

@@ -38,6 +38,10 @@ namespace dbsde {
 
 constexpr int P3_WAVES = 4;
 constexpr int P3_ROWS = 16 * P3_WAVES;
+// split-bf16 weight ring depth: 3 pieces of 21 KiB (T = 7) per workgroup, two
+// workgroups per CU (measured: 8-wave 128-row workgroups with a 6-deep ring,
+// one per CU, 0.359 vs 0.310 ms for the phases, profiles/r3_ab_ring.txt)
+constexpr int P3_NBUF_X3 = 3;
 
 // B-operand-layout tile <-> row-major global matrix (float4 per 16-col block)
 template <int TT>
@@ -164,19 +168,20 @@ __device__ __forceinline__ void sgemm_piece(Mat<TO>& acc, const Mat<TI>& b, cons
   }
 }
 
-// wave w copies fragments w, w + 4, ... of an nf-fragment piece
+// wave w copies fragments w, w + P3_WAVES, ... of an nf-fragment piece
 __device__ __forceinline__ void piece_dma(const float* img, int nf, floatx4* buf, int wave, int lane) {
   for (int f = wave; f < nf; f += P3_WAVES) glds16(img + (size_t)f * 256 + lane * 4, buf + f * 64);
 }
 
 // piece sequencer: wait for this piece, publish it, start the one NBUF - 1
 // ahead (NBUF-buffer LDS ring; the fp32 kernels use 2, the split-bf16 kernels,
-// whose pieces carry 1/4 of the MFMA work, 3).
+// whose pieces carry 1/4 of the MFMA work, P3_NBUF_X3).
 // NYOUNG = vector-memory operations this wave is guaranteed to have issued
 // after the piece's DMA (deferred stores, early loads): they may stay in flight
 // across the barrier.  Under-counting is safe, over-counting is a race.  With
-// NBUF = 3 the DMA of the following piece was also issued after this piece's:
-// LC = a lower bound of this wave's chunks of it (waves copy 5 or 6 of 21).
+// NBUF > 2 the DMAs of the k = min(NBUF - 2, n - 1 - st) following pieces were
+// also issued after this piece's: LC = a lower bound of this wave's chunks of
+// each (waves copy 5 or 6 of 21), so k LC more may stay in flight.
 template <int NBUF, int LC>
 struct PieceStagerT {
   floatx4* wl;
@@ -189,13 +194,23 @@ struct PieceStagerT {
     for (int k = 0; k < NBUF - 1; ++k)
       if (k < n) piece_dma(img[k], nf[k], wl + k * buf, wave, lane);
   }
+  // vm_wait<NYOUNG + LC k> for the runtime k (uniform) of younger pieces
+  template <int NYOUNG, int K>
+  __device__ __forceinline__ void wait_younger(int k) {
+    if constexpr (K == 0) {
+      vm_wait<NYOUNG>();
+    } else {
+      if (k >= K)
+        vm_wait<NYOUNG + LC * K>();
+      else
+        wait_younger<NYOUNG, K - 1>(k);
+    }
+  }
   template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
     if constexpr (NBUF > 2) {
-      if (st + 1 < n)
-        vm_wait<NYOUNG + LC>();
-      else
-        vm_wait<NYOUNG>();
+      const int k = min(NBUF - 2, n - 1 - st);
+      wait_younger<NYOUNG, NBUF - 2>(k);
     } else {
       vm_wait<NYOUNG>();
     }
@@ -211,7 +226,7 @@ struct PieceStagerT {
 };
 // the kernels' stager: X3 pieces are 3 TO chunks, TO >= min(T, TD)
 template <bool X3, int T, int TD>
-using PieceStager = PieceStagerT<X3 ? 3 : 2, X3 ? (3 * (T < TD ? T : TD)) / P3_WAVES : 0>;
+using PieceStager = PieceStagerT<X3 ? P3_NBUF_X3 : 2, X3 ? (3 * (T < TD ? T : TD)) / P3_WAVES : 0>;
 
 
 struct NoOp {
@@ -393,10 +408,10 @@ __device__ __forceinline__ void stage_mm(Mat<TO>& acc, const Mat<TI>& b, SG& sg,
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, {[Z_j], B_j} j=K..1, Z0
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT, bool HV, bool X3>
-__global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseA_kernel(FusedArgs p) {
+__global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel(FusedArgs p) {
   constexpr bool PFA = true;    // group-ahead fragment prefetch (sgemm_piece)
   constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
-  __shared__ floatx4 wl[(X3 ? 3 : 2) * BUF];
+  __shared__ floatx4 wl[(X3 ? P3_NBUF_X3 : 2) * BUF];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = blockIdx.x + p.tile0;   // 64-row tile (chunked launches offset it)
@@ -556,12 +571,12 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseA_kernel(FusedArgs p) {
 // stage images (host order): X0, {F_j, [X_j]} j=1..K, B_j j=K..1
 // ---------------------------------------------------------------------------
 template <int T, int TD, int K, int ACT, bool HV, bool X3>
-__global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseC_kernel(FusedArgs p) {
+__global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel(FusedArgs p) {
   // prefetch in the tangent / reverse stages (the split-bf16 form is at the
   // register limit without it)
   constexpr bool PFC_T = !X3 || (HV && ACT != ACT_TANH), PFC_R = false;   // tanh: register-bound
   constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
-  __shared__ floatx4 wl[(X3 ? 3 : 2) * BUF];
+  __shared__ floatx4 wl[(X3 ? P3_NBUF_X3 : 2) * BUF];
   __shared__ double lsum[P3_WAVES];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

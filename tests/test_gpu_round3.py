@@ -359,6 +359,6 @@ def test_fused_update_equals_separate_optimizer(pkg, dev, name):
         b.solver.loss_grad(b.params, b.M, b.N, b._device_xi(0, b.M), seed=s, grad=b.grad, loss=b._gradbuf[-1:])
         b._update(ob)                                                      # separate launches
     torch.cuda.synchronize()
-    assert torch.equal(a.params, b.params)
-    assert torch.equal(oa["m"], ob["m"]) and torch.equal(oa["v"], ob["v"])
+    for x, y in ((a.params, b.params), (oa["m"], ob["m"]), (oa["v"], ob["v"])):   # (ASGD diverges to NaN here)
+        torch.testing.assert_close(x, y, rtol=0, atol=0, equal_nan=True)
     assert a.optimizer_steps_taken(oa) == b.optimizer_steps_taken(ob) == 3
