@@ -829,6 +829,21 @@ RolloutArgs rollout_args(dbsde_ctx* c, const dbsde_batch* b) {
   return ra;
 }
 
+// the correlated path kernel for ceil(nb / 16) output blocks
+void launch_corr(const RolloutArgs& ra, hipStream_t s) {
+  const dim3 g((ra.M + CP_PATHS - 1) / CP_PATHS);
+  switch ((ra.nb + 15) / 16) {
+    case 1: rollout_corr_kernel<1><<<g, 256, 0, s>>>(ra); break;
+    case 2: rollout_corr_kernel<2><<<g, 256, 0, s>>>(ra); break;
+    case 3: rollout_corr_kernel<3><<<g, 256, 0, s>>>(ra); break;
+    case 4: rollout_corr_kernel<4><<<g, 256, 0, s>>>(ra); break;
+    case 5: rollout_corr_kernel<5><<<g, 256, 0, s>>>(ra); break;
+    case 6: rollout_corr_kernel<6><<<g, 256, 0, s>>>(ra); break;
+    case 7: rollout_corr_kernel<7><<<g, 256, 0, s>>>(ra); break;
+    default: rollout_corr_kernel<8><<<g, 256, 0, s>>>(ra); break;
+  }
+}
+
 // Euler-Maruyama paths (ra.out == PATH_ROLLOUT) or the device fetch_minibatch
 // (PATH_FETCH_*): Heston, Cholesky-correlated device mode, or diagonal
 int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
@@ -840,10 +855,8 @@ int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
     const int nthr = ra.M * ra.nb;
     RUN(c, name, 0.0, bytes, rollout_heston_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
   } else if (c->Lt && !ra.W) {
-    const int G = (ra.nb + 63) / 64 * 64, PB = (256 / G) * CP_PPT;
-    const size_t smem = ((size_t)((ra.nb * ra.nb + 3) & ~3) + 2 * (size_t)ra.nb * PB) * sizeof(float);
     RUN(c, name, 2.0 * steps * ra.nb * ra.nb / 2, bytes,
-        rollout_corr_kernel<<<(ra.M + PB - 1) / PB, 256, smem, s>>>(ra));
+        launch_corr(ra, s));
   } else {
     const int nthr = ra.M * ra.D;
     RUN(c, name, 0.0, bytes, rollout_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));

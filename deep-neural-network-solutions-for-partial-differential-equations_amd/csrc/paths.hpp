@@ -163,119 +163,176 @@ __global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
 }
 
 // --------------------------------------------------------------------------
-// Cholesky-correlated device mode (with_corr...py:339-341: dW = L (sqrt(dt) z)):
-// L^T staged in LDS once per workgroup, the uncorrelated increments of all
-// paths of the workgroup staged per step, dW_d = sum_{k<=d} L[d][k] dwu_k as a
-// VALU dot product per (path, d): one lane-distinct LDS read of L^T[k][d]
-// (consecutive d -> conflict-free) and one broadcast 16-byte read of the
-// four paths' dwu_k feed four FMAs.  Then the diagonal Euler step.
-// Threads: G = 64 ceil(nb/64) per path group, 256/G groups, CP_PPT paths per
-// thread.  nb <= 128.
+// Cholesky-correlated device mode (with_corr...py:339-341: dW = L (sqrt(dt) z))
+// with the correlation product on the matrix cores: per step n the increments
+// of a 16-path group are dW^T = L . xi^T, one v_mfma_f32_16x16x4_f32 per
+// (16-dim output block o, 4-dim input step t) -- A = L (constant, held in
+// registers for the whole rollout), B = xi (this step's uncorrelated
+// sqrt(dt) z of the 16 paths, staged in LDS).  L is lower triangular, so block
+// o stops at t < 4 o + 4.  The MFMA output layout (lane (cl, q): path cl, dims
+// 16 o + 4 q + r) is the layout the Euler step and the xin / sdw rows need, so
+// the step runs straight out of the accumulators.
+// Workgroup = 16 paths, 4 waves; wave w owns output blocks w and nblk-1-w
+// (equal triangular cost per wave).  The Philox draws of the next 4-step
+// block (4 normals per (path, dim) call) are made by all 256 threads into the
+// other LDS buffer while this block's steps run.  nb <= 128.
+// LDS: xi[buf][k][q][p][t] (dim 4 t + q of path p at step 4 blk + k), t
+// padded to 36 floats: the 16 paths of one q read 16-byte slots 36 floats
+// apart = distinct 4-bank groups (conflict-free ds_read_b128).
 // --------------------------------------------------------------------------
-constexpr int CP_PPT = 4;
 constexpr int CP_NBMAX = 128;
+constexpr int CP_PATHS = 16;
+constexpr int CP_TS = 36;
+constexpr int CP_BUF = 4 * 4 * CP_PATHS * CP_TS;   // floats per 4-step buffer
 
-__global__ void __launch_bounds__(256) rollout_corr_kernel(RolloutArgs p) {
-  extern __shared__ float smem[];
-  const int nb = p.nb;
-  const int G = (nb + 63) / 64 * 64, NG = 256 / G, PB = NG * CP_PPT;   // paths per block
-  float* Lt = smem;                          // [nb][nb]
-  float* zs = smem + ((nb * nb + 3) & ~3);    // [2][nb][PB], 16-byte aligned
-  for (int i = threadIdx.x; i < nb * nb; i += 256) Lt[i] = p.Lt[i];
-  const int tid = threadIdx.x, d = tid % G, grp = tid / G;
-  const bool active_d = d < nb && grp < NG;
-  const int wave_last = min(nb - 1, (tid / 64) * 64 % G + 63);   // largest d of this wave
-  const int kmax = wave_last + 1;
-  const int N1 = p.N + 1;
-  const double dt64 = (double)p.T / (double)p.N;
+typedef float cpf4 __attribute__((ext_vector_type(4)));
+
+// the uncorrelated sqrt(dt) z of step block sb (steps 4 sb .. 4 sb + 3) of the
+// workgroup's 16 paths into one LDS buffer: item (path, dim) -> 4 steps
+__device__ __forceinline__ void corr_draw(const RolloutArgs& p, int m0, int nt4, float sqdt, int sb, float* xb) {
+  for (int it = threadIdx.x; it < CP_PATHS * 4 * nt4; it += 256) {
+    const int pp = it & (CP_PATHS - 1), d = it >> 4;
+    const int m = m0 + pp;
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    if (d < p.nb && m < p.M) philox_normal4(p.seed, p.offset, (uint32_t)(p.path0 + m), (uint32_t)sb, (uint32_t)d, z);
+    const int qq = d & 3, t = d >> 2;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xb[((k * 4 + qq) * CP_PATHS + pp) * CP_TS + t] = sqdt * z[k];
+  }
+}
+
+// one wave's share: output blocks O1 and O2 (O2 < 0: none; O1 < 0: the wave
+// only draws), K-steps t < 4 O + 4 (the lower triangle; L is zero-padded past
+// nb), everything compile-time so the L fragments stay in registers
+template <int O1, int O2>
+__device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs) {
+  constexpr int NO = (O1 >= 0) + (O2 >= 0);
+  constexpr int T1 = O1 >= 0 ? 4 * O1 + 4 : 0, T2 = O2 >= 0 ? 4 * O2 + 4 : 0;
+  constexpr int TM = T1 > T2 ? T1 : T2;
+  const int nb = p.nb, nt4 = (nb + 3) / 4;
+  const int lane = threadIdx.x & 63, cl = lane & 15, q = lane >> 4;
+  const int m0 = blockIdx.x * CP_PATHS;
+  const int N1 = p.N + 1, nsb = (p.N + 3) / 4;
   const float sqdt = sqrtf(p.T / (float)p.N);
-  int mi[CP_PPT];
-  bool ok[CP_PPT];
-  float x[CP_PPT];
-  FetchAcc fa[CP_PPT];
+  const double dt64 = (double)p.T / (double)p.N;
+  const int ob[2] = {O1, O2};
+  // A fragments: L[16 o + cl][4 t + q] (zero outside the lower triangle / nb)
+  float la1[T1 > 0 ? T1 : 1], la2[T2 > 0 ? T2 : 1];
 #pragma unroll
-  for (int i = 0; i < CP_PPT; ++i) {
-    mi[i] = blockIdx.x * PB + grp * CP_PPT + i;
-    ok[i] = active_d && mi[i] < p.M;
-    x[i] = ok[i] ? p.Xi[(p.xi_rows == 1 ? 0 : mi[i]) * p.D + d] : 0.f;
+  for (int t = 0; t < T1; ++t) {
+    const int d = 16 * O1 + cl, k = 4 * t + q;
+    la1[t] = (d < nb && k <= d && k < nb) ? p.Lt[(size_t)k * nb + d] : 0.f;
   }
+#pragma unroll
+  for (int t = 0; t < T2; ++t) {
+    const int d = 16 * O2 + cl, k = 4 * t + q;
+    la2[t] = (d < nb && k <= d && k < nb) ? p.Lt[(size_t)k * nb + d] : 0.f;
+  }
+  const int m = m0 + cl;
+  const bool ok = m < p.M;
+  float x[2][4];
+  FetchAcc fa[2][4];
+  float t0 = (p.t && ok) ? p.t[(size_t)m * N1] : 0.f;
+#pragma unroll
+  for (int oc = 0; oc < NO; ++oc)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int d = 16 * ob[oc] + 4 * q + r;
+      const bool own = d < nb && ok;
+      x[oc][r] = own ? p.Xi[(p.xi_rows == 1 ? 0 : m) * p.D + d] : 0.f;
+      if (own && p.out != PATH_ROLLOUT) fa[oc][r].put(p, m, d, 0, t0, 0.f);
+    }
+  const bool writes_t = O1 == 0 && q == 0 && ok;   // columns 0 (t) and D + 1 (1)
   double tacc = 0.0;
-  // time grid: the caller's t [M, N+1] when given (as step_block), else the
-  // reference's fp32(fp64 cumsum of T/N)
-  float t0[CP_PPT];
-#pragma unroll
-  for (int i = 0; i < CP_PPT; ++i) {
-    t0[i] = (p.t && ok[i]) ? p.t[(size_t)mi[i] * N1] : 0.f;
-    if (ok[i] && p.out != PATH_ROLLOUT) fa[i].put(p, mi[i], d, 0, t0[i], 0.f);
-  }
-  int buf = 0;
-  for (int n0 = 0; n0 < p.N; n0 += 4) {
-    float z[CP_PPT][4];
-#pragma unroll
-    for (int i = 0; i < CP_PPT; ++i) {
-      if (ok[i]) philox_normal4(p.seed, p.offset, (uint32_t)(p.path0 + mi[i]), (uint32_t)(n0 >> 2), (uint32_t)d, z[i]);
-      else z[i][0] = z[i][1] = z[i][2] = z[i][3] = 0.f;
-    }
-    for (int k4 = 0; k4 < 4 && n0 + k4 < p.N; ++k4) {
-      const int n = n0 + k4;
-      if (active_d) {
-#pragma unroll
-        for (int i = 0; i < CP_PPT; ++i) zs[(buf * nb + d) * PB + grp * CP_PPT + i] = sqdt * z[i][k4];
-      }
+  // the K-steps past nb (t >= nt4 up to 4 O + 4) read slots no draw writes:
+  // zero both buffers once (0 * stale LDS could be NaN)
+  for (int i = threadIdx.x; i < 2 * CP_BUF; i += 256) xs[i] = 0.f;
+  __syncthreads();
+  corr_draw(p, m0, nt4, sqdt, 0, xs);
+  __syncthreads();
+  for (int sb = 0; sb < nsb; ++sb) {
+    if (sb + 1 < nsb) corr_draw(p, m0, nt4, sqdt, sb + 1, xs + ((sb + 1) & 1) * CP_BUF);
+    const float* xb = xs + (sb & 1) * CP_BUF;
+    for (int k = 0; k < 4; ++k) {
+      const int n = 4 * sb + k;
+      if (n >= p.N) break;
       tacc += dt64;
-      float t1[CP_PPT];
+      const float t1 = (p.t && ok) ? p.t[(size_t)m * N1 + n + 1] : (float)tacc;
+      if constexpr (NO > 0) {
+        const float* xr = xb + ((k * 4 + q) * CP_PATHS + cl) * CP_TS;
+        cpf4 acc[2] = {cpf4{0.f, 0.f, 0.f, 0.f}, cpf4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int i = 0; i < CP_PPT; ++i) t1[i] = (p.t && ok[i]) ? p.t[(size_t)mi[i] * N1 + n + 1] : (float)tacc;
-      __syncthreads();
-      float acc[CP_PPT] = {};
-      if (active_d) {
-        const float* zb = zs + (size_t)buf * nb * PB + grp * CP_PPT;
-        for (int k = 0; k < kmax; ++k) {
-          const float l = Lt[k * nb + d];
-          const float4 zz = *(const float4*)(zb + k * PB);
-          acc[0] = fmaf(l, zz.x, acc[0]);
-          acc[1] = fmaf(l, zz.y, acc[1]);
-          acc[2] = fmaf(l, zz.z, acc[2]);
-          acc[3] = fmaf(l, zz.w, acc[3]);
+        for (int s4 = 0; s4 < TM / 4; ++s4) {
+          const cpf4 bz = *(const cpf4*)(xr + 4 * s4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int t = 4 * s4 + j;
+            if (t < T1) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(la1[t < T1 ? t : 0], bz[j], acc[0], 0, 0, 0);
+            if (t < T2) acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(la2[t < T2 ? t : 0], bz[j], acc[1], 0, 0, 0);
+          }
+        }
+        const size_t row = (size_t)m * N1 + n;
+        const float dt = rn_sub(t1, t0);
+#pragma unroll
+        for (int oc = 0; oc < NO; ++oc)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int d = 16 * ob[oc] + 4 * q + r;
+            if (d >= nb || !ok) continue;
+            const float dw = acc[oc][r];
+            if (p.out != PATH_ROLLOUT) {
+              fa[oc][r].put(p, m, d, n + 1, t1, dw);
+              continue;
+            }
+            p.xin[row * p.ldx + 1 + d] = x[oc][r];
+            const float sg = rn_add(rn_mul(p.sig_a, x[oc][r]), p.sig_b);
+            const float sv = rn_mul(sg, dw);
+            p.sdw[row * p.ldx + 1 + d] = sv;
+            x[oc][r] = rn_add(rn_add(x[oc][r], rn_mul(rn_mul(p.mu_a, x[oc][r]), dt)), sv);
+          }
+        if (writes_t && p.out == PATH_ROLLOUT) {
+          p.xin[row * p.ldx] = t0;
+          p.xin[row * p.ldx + p.D + 1] = 1.0f;
         }
       }
-      buf ^= 1;
+      t0 = t1;
+    }
+    __syncthreads();
+  }
+  if constexpr (NO > 0) {
+    if (p.out != PATH_ROLLOUT || !ok) return;
+    const size_t row = (size_t)m * N1 + p.N;
 #pragma unroll
-      for (int i = 0; i < CP_PPT; ++i) {
-        if (!ok[i]) continue;
-        if (p.out != PATH_ROLLOUT) {
-          fa[i].put(p, mi[i], d, n + 1, t1[i], acc[i]);
-          continue;
-        }
-        const size_t r = (size_t)mi[i] * N1 + n;
-        float* xr = p.xin + r * p.ldx;
-        xr[1 + d] = x[i];
-        if (d == 0) {
-          xr[0] = t0[i];
-          xr[p.D + 1] = 1.0f;
-        }
-        const float dt = rn_sub(t1[i], t0[i]);
-        const float sg = rn_add(rn_mul(p.sig_a, x[i]), p.sig_b);
-        const float s = rn_mul(sg, acc[i]);
-        p.sdw[r * p.ldx + 1 + d] = s;
-        x[i] = rn_add(rn_add(x[i], rn_mul(rn_mul(p.mu_a, x[i]), dt)), s);
+    for (int oc = 0; oc < NO; ++oc)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int d = 16 * ob[oc] + 4 * q + r;
+        if (d >= nb) continue;
+        p.xin[row * p.ldx + 1 + d] = x[oc][r];
+        p.sdw[row * p.ldx + 1 + d] = 0.0f;
       }
-#pragma unroll
-      for (int i = 0; i < CP_PPT; ++i) t0[i] = t1[i];
+    if (writes_t) {
+      p.xin[row * p.ldx] = t0;
+      p.xin[row * p.ldx + p.D + 1] = 1.0f;
     }
   }
-  if (p.out != PATH_ROLLOUT) return;
-#pragma unroll
-  for (int i = 0; i < CP_PPT; ++i) {
-    if (!ok[i]) continue;
-    const size_t r = (size_t)mi[i] * N1 + p.N;
-    float* xr = p.xin + r * p.ldx;
-    xr[1 + d] = x[i];
-    p.sdw[r * p.ldx + 1 + d] = 0.0f;
-    if (d == 0) {
-      xr[0] = t0[i];
-      xr[p.D + 1] = 1.0f;
-    }
+}
+
+// wave w owns output blocks w and NBLK - 1 - w (equal triangular cost)
+template <int NBLK>
+__global__ void __launch_bounds__(256) rollout_corr_kernel(RolloutArgs p) {
+  __shared__ __attribute__((aligned(16))) float xs[2 * CP_BUF];
+  constexpr int H = (NBLK + 1) / 2;
+  constexpr int A0 = 0 < H ? 0 : -1, A1 = 1 < H ? 1 : -1, A2 = 2 < H ? 2 : -1, A3 = 3 < H ? 3 : -1;
+  constexpr int B0 = (A0 >= 0 && NBLK - 1 > 0) ? NBLK - 1 : -1;
+  constexpr int B1 = (A1 >= 0 && NBLK - 2 > 1) ? NBLK - 2 : -1;
+  constexpr int B2 = (A2 >= 0 && NBLK - 3 > 2) ? NBLK - 3 : -1;
+  constexpr int B3 = (A3 >= 0 && NBLK - 4 > 3) ? NBLK - 4 : -1;
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
+    case 0: corr_wave<A0, B0>(p, xs); break;
+    case 1: corr_wave<A1, B1>(p, xs); break;
+    case 2: corr_wave<A2, B2>(p, xs); break;
+    default: corr_wave<A3, B3>(p, xs); break;
   }
 }
 

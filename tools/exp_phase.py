@@ -85,6 +85,26 @@ def edit(src, name):
             sig = "__device__ __forceinline__ void %s(Mat<TT>& m, const float* base, int ld, int row0, int col0) {" % fn
             assert sig in src, fn
             src = src.replace(sig, sig + "\n  if (ld > 0) { for (int t = 0; t < TT; ++t) m.v[t] = floatx4{0.f, 0.f, 0.f, 0.f}; return; }")
+    if name in ("stamps2", "stamps3"):   # per-wave s_memtime sums: piece vmcnt wait, barrier wait, kernel total (printf)
+        a = "  __device__ __forceinline__ const floatx4* next() {\n"
+        assert a in src
+        src = src.replace("  int n, st, wave, lane, buf;\n", "  int n, st, wave, lane, buf;\n  unsigned long long tvm = 0, tbar = 0;\n")
+        src = src.replace("      wait_younger<NYOUNG, NBUF - 2>(k);\n    } else {\n      vm_wait<NYOUNG>();\n    }\n    lds_barrier();\n",
+                          "      const unsigned long long ta = __builtin_amdgcn_s_memtime();\n      wait_younger<NYOUNG, NBUF - 2>(k);\n"
+                          "      const unsigned long long tb = __builtin_amdgcn_s_memtime();\n      lds_barrier();\n"
+                          "      const unsigned long long tc = __builtin_amdgcn_s_memtime();\n      tvm += tb - ta; tbar += tc - tb;\n"
+                          "    } else {\n      vm_wait<NYOUNG>();\n      lds_barrier();\n    }\n")
+        for kern, tag in (("phaseA_kernel(FusedArgs p) {\n", "A"), ("phaseC_kernel(FusedArgs p) {\n", "C")):
+            i = src.index(kern) + len(kern)
+            src = src[:i] + "  const unsigned long long t_start = __builtin_amdgcn_s_memtime();\n" + src[i:]
+        # kernel ends: the closing brace before the phase C comment / the namespace end
+        endA = src.index("// phase C: cotangents")
+        j = src.rindex("}\n", 0, endA)
+        sel = "(blockIdx.x % 50) == 0" if name == "stamps2" else "threadIdx.x == 0"
+        src = src[:j] + ('  if ((threadIdx.x & 63) == 0 && ' + sel + ') printf("STAMP A tile0=%d wg=%d wave=%d hw=%u xcc=%u t0=%llu total=%llu vm=%llu bar=%llu\\n", p.tile0, (int)blockIdx.x, wave, __builtin_amdgcn_s_getreg(63492), __builtin_amdgcn_s_getreg(63508), t_start, __builtin_amdgcn_s_memtime() - t_start, sg.tvm, sg.tbar);\n') + src[j:]
+        endC = src.index("}  // namespace dbsde")
+        j = src.rindex("}\n", 0, endC)
+        src = src[:j] + ('  if ((threadIdx.x & 63) == 0 && ' + sel + ') printf("STAMP C tile0=%d wg=%d wave=%d hw=%u xcc=%u t0=%llu total=%llu vm=%llu bar=%llu\\n", p.tile0, (int)blockIdx.x, wave, __builtin_amdgcn_s_getreg(63492), __builtin_amdgcn_s_getreg(63508), t_start, __builtin_amdgcn_s_memtime() - t_start, sg.tvm, sg.tbar);\n') + src[j:]
     if name in ("nostage", "bare", "bareall"):
         src = src.replace("  __device__ __forceinline__ const floatx4* next() {\n",
                           "  __device__ __forceinline__ const floatx4* next() {\n"
@@ -110,7 +130,17 @@ def build(name):
     ph = os.path.join(csrc, "phase.hpp")
     s = open(ph).read()
     defs = []
-    if name == "stamps":    # per-piece s_memtime printf of three tiles (diagnostic build)
+    eng_edits = {   # engine.hip launch-shape variants
+        "onechunk": ("  int chunks = 2;", "  int chunks = 1;"),    # all of phase A, then all of phase C
+        "onepipe": ("  int pipes = 2;", "  int pipes = 1;"),       # A0 C0 A1 C1 in order on one stream
+    }
+    if name in eng_edits:
+        ep = os.path.join(csrc, "engine.hip")
+        e = open(ep).read()
+        a, b = eng_edits[name]
+        assert a in e, name
+        open(ep, "w").write(e.replace(a, b))
+    elif name == "stamps":    # per-piece s_memtime printf of three tiles (diagnostic build)
         defs = ["-DDBSDE_STAMPS"]
     elif name == "noslp":   # no SLP packing of f32 elementwise work into v_pk_* (MI355X_MICROARCH: anti-lever beside MFMA)
         defs = ["-fno-slp-vectorize"]
