@@ -26,6 +26,7 @@
 #include "paths.hpp"
 #include "phase.hpp"
 #include "chainx3.hpp"
+#include "tnx3.hpp"
 #include "tnw.hpp"
 #include "vec.hpp"
 
@@ -833,14 +834,14 @@ RolloutArgs rollout_args(dbsde_ctx* c, const dbsde_batch* b) {
 void launch_corr(const RolloutArgs& ra, hipStream_t s) {
   const dim3 g((ra.M + CP_PATHS - 1) / CP_PATHS);
   switch ((ra.nb + 15) / 16) {
-    case 1: rollout_corr_kernel<1><<<g, 256, 0, s>>>(ra); break;
-    case 2: rollout_corr_kernel<2><<<g, 256, 0, s>>>(ra); break;
-    case 3: rollout_corr_kernel<3><<<g, 256, 0, s>>>(ra); break;
-    case 4: rollout_corr_kernel<4><<<g, 256, 0, s>>>(ra); break;
-    case 5: rollout_corr_kernel<5><<<g, 256, 0, s>>>(ra); break;
-    case 6: rollout_corr_kernel<6><<<g, 256, 0, s>>>(ra); break;
-    case 7: rollout_corr_kernel<7><<<g, 256, 0, s>>>(ra); break;
-    default: rollout_corr_kernel<8><<<g, 256, 0, s>>>(ra); break;
+    case 1: rollout_corr_kernel<1><<<g, CP_THREADS, 0, s>>>(ra); break;
+    case 2: rollout_corr_kernel<2><<<g, CP_THREADS, 0, s>>>(ra); break;
+    case 3: rollout_corr_kernel<3><<<g, CP_THREADS, 0, s>>>(ra); break;
+    case 4: rollout_corr_kernel<4><<<g, CP_THREADS, 0, s>>>(ra); break;
+    case 5: rollout_corr_kernel<5><<<g, CP_THREADS, 0, s>>>(ra); break;
+    case 6: rollout_corr_kernel<6><<<g, CP_THREADS, 0, s>>>(ra); break;
+    case 7: rollout_corr_kernel<7><<<g, CP_THREADS, 0, s>>>(ra); break;
+    default: rollout_corr_kernel<8><<<g, CP_THREADS, 0, s>>>(ra); break;
   }
 }
 
@@ -1847,7 +1848,22 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       tfl += 2.0 * 2.0 * R * (L[K + 1] + 1);
     }
     if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
-    RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
+    if (c->x3chain) {
+      // split-bf16 tiles for the layer problems (tnx3.hpp), the fp32 kernel
+      // for the one-row output layer
+      int maxt3 = 0;
+      for (int j = 0; j <= K; ++j)
+        maxt3 = std::max(maxt3, ((ta.prob[j].nA[0] + TX_TILE - 1) / TX_TILE) * ((ta.prob[j].nB[0] + TX_TILE - 1) / TX_TILE));
+      const int rps32 = ((Rp + S_ - 1) / S_ + 31) / 32 * 32;
+      if (Rp % 32 != 0) return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
+      TNArgs to = ta;
+      to.prob[0] = ta.prob[K + 1];
+      RUN(c, "tn_weight_grad", tfl, 0.0,
+          tn_x3_kernel<<<dim3(maxt3, (Rp + rps32 - 1) / rps32, K + 1), 256, 0, s>>>(ta, rps32);
+          tn_gemm_kernel<<<dim3(ta.prob[K + 1].mt * ta.prob[K + 1].nt, S_, 1), 256, 0, s>>>(to));
+    } else {
+      RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
+    }
     if ((rc = finalize_grads(c, params, grad, nullptr, 0, nullptr, fo))) return rc;
     }
   }

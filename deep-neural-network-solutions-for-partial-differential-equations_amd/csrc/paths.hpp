@@ -172,10 +172,11 @@ __global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
 // o stops at t < 4 o + 4.  The MFMA output layout (lane (cl, q): path cl, dims
 // 16 o + 4 q + r) is the layout the Euler step and the xin / sdw rows need, so
 // the step runs straight out of the accumulators.
-// Workgroup = 16 paths, 4 waves; wave w owns output blocks w and nblk-1-w
-// (equal triangular cost per wave).  The Philox draws of the next 4-step
-// block (4 normals per (path, dim) call) are made by all 256 threads into the
-// other LDS buffer while this block's steps run.  nb <= 128.
+// Workgroup = 16 paths, 8 waves (two per SIMD); wave w < nblk owns output
+// block w, with its K-sum in two independent accumulation chains (the
+// dependent-accumulator latency bounds a step, not the issue rate).  The
+// Philox draws of the next 4-step block (4 normals per (path, dim) call) are
+// made by all 512 threads into the other LDS buffer.  nb <= 128.
 // LDS: xi[buf][k][q][p][t] (dim 4 t + q of path p at step 4 blk + k), t
 // padded to 36 floats: the 16 paths of one q read 16-byte slots 36 floats
 // apart = distinct 4-bank groups (conflict-free ds_read_b128).
@@ -184,13 +185,14 @@ constexpr int CP_NBMAX = 128;
 constexpr int CP_PATHS = 16;
 constexpr int CP_TS = 36;
 constexpr int CP_BUF = 4 * 4 * CP_PATHS * CP_TS;   // floats per 4-step buffer
+constexpr int CP_THREADS = 512;                     // 8 waves: one per output block, the rest draw
 
 typedef float cpf4 __attribute__((ext_vector_type(4)));
 
 // the uncorrelated sqrt(dt) z of step block sb (steps 4 sb .. 4 sb + 3) of the
 // workgroup's 16 paths into one LDS buffer: item (path, dim) -> 4 steps
 __device__ __forceinline__ void corr_draw(const RolloutArgs& p, int m0, int nt4, float sqdt, int sb, float* xb) {
-  for (int it = threadIdx.x; it < CP_PATHS * 4 * nt4; it += 256) {
+  for (int it = threadIdx.x; it < CP_PATHS * 4 * nt4; it += CP_THREADS) {
     const int pp = it & (CP_PATHS - 1), d = it >> 4;
     const int m = m0 + pp;
     float z[4] = {0.f, 0.f, 0.f, 0.f};
@@ -246,7 +248,7 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs) {
   double tacc = 0.0;
   // the K-steps past nb (t >= nt4 up to 4 O + 4) read slots no draw writes:
   // zero both buffers once (0 * stale LDS could be NaN)
-  for (int i = threadIdx.x; i < 2 * CP_BUF; i += 256) xs[i] = 0.f;
+  for (int i = threadIdx.x; i < 2 * CP_BUF; i += CP_THREADS) xs[i] = 0.f;
   __syncthreads();
   corr_draw(p, m0, nt4, sqdt, 0, xs);
   __syncthreads();
@@ -260,17 +262,25 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs) {
       const float t1 = (p.t && ok) ? p.t[(size_t)m * N1 + n + 1] : (float)tacc;
       if constexpr (NO > 0) {
         const float* xr = xb + ((k * 4 + q) * CP_PATHS + cl) * CP_TS;
-        cpf4 acc[2] = {cpf4{0.f, 0.f, 0.f, 0.f}, cpf4{0.f, 0.f, 0.f, 0.f}};
+        // two independent accumulation chains per block (even / odd K-steps):
+        // the dependent-accumulator latency, not the issue rate, bounds a step
+        cpf4 acc[2], acc2[2];
+#pragma unroll
+        for (int oc = 0; oc < 2; ++oc) acc[oc] = acc2[oc] = cpf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s4 = 0; s4 < TM / 4; ++s4) {
           const cpf4 bz = *(const cpf4*)(xr + 4 * s4);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int t = 4 * s4 + j;
-            if (t < T1) acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(la1[t < T1 ? t : 0], bz[j], acc[0], 0, 0, 0);
-            if (t < T2) acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(la2[t < T2 ? t : 0], bz[j], acc[1], 0, 0, 0);
+            cpf4& a1 = (j & 1) ? acc2[0] : acc[0];
+            cpf4& a2 = (j & 1) ? acc2[1] : acc[1];
+            if (t < T1) a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(la1[t < T1 ? t : 0], bz[j], a1, 0, 0, 0);
+            if (t < T2) a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(la2[t < T2 ? t : 0], bz[j], a2, 0, 0, 0);
           }
         }
+#pragma unroll
+        for (int oc = 0; oc < 2; ++oc) acc[oc] += acc2[oc];
         const size_t row = (size_t)m * N1 + n;
         const float dt = rn_sub(t1, t0);
 #pragma unroll
@@ -318,21 +328,19 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs) {
   }
 }
 
-// wave w owns output blocks w and NBLK - 1 - w (equal triangular cost)
+// wave w < NBLK owns output block w; all 8 waves draw
 template <int NBLK>
-__global__ void __launch_bounds__(256) rollout_corr_kernel(RolloutArgs p) {
+__global__ void __launch_bounds__(CP_THREADS) rollout_corr_kernel(RolloutArgs p) {
   __shared__ __attribute__((aligned(16))) float xs[2 * CP_BUF];
-  constexpr int H = (NBLK + 1) / 2;
-  constexpr int A0 = 0 < H ? 0 : -1, A1 = 1 < H ? 1 : -1, A2 = 2 < H ? 2 : -1, A3 = 3 < H ? 3 : -1;
-  constexpr int B0 = (A0 >= 0 && NBLK - 1 > 0) ? NBLK - 1 : -1;
-  constexpr int B1 = (A1 >= 0 && NBLK - 2 > 1) ? NBLK - 2 : -1;
-  constexpr int B2 = (A2 >= 0 && NBLK - 3 > 2) ? NBLK - 3 : -1;
-  constexpr int B3 = (A3 >= 0 && NBLK - 4 > 3) ? NBLK - 4 : -1;
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: corr_wave<A0, B0>(p, xs); break;
-    case 1: corr_wave<A1, B1>(p, xs); break;
-    case 2: corr_wave<A2, B2>(p, xs); break;
-    default: corr_wave<A3, B3>(p, xs); break;
+    case 0: corr_wave<0, -1>(p, xs); break;
+    case 1: corr_wave<(1 < NBLK ? 1 : -1), -1>(p, xs); break;
+    case 2: corr_wave<(2 < NBLK ? 2 : -1), -1>(p, xs); break;
+    case 3: corr_wave<(3 < NBLK ? 3 : -1), -1>(p, xs); break;
+    case 4: corr_wave<(4 < NBLK ? 4 : -1), -1>(p, xs); break;
+    case 5: corr_wave<(5 < NBLK ? 5 : -1), -1>(p, xs); break;
+    case 6: corr_wave<(6 < NBLK ? 6 : -1), -1>(p, xs); break;
+    default: corr_wave<(7 < NBLK ? 7 : -1), -1>(p, xs); break;
   }
 }
 

@@ -105,6 +105,45 @@ def edit(src, name):
         endC = src.index("}  // namespace dbsde")
         j = src.rindex("}\n", 0, endC)
         src = src[:j] + ('  if ((threadIdx.x & 63) == 0 && ' + sel + ') printf("STAMP C tile0=%d wg=%d wave=%d hw=%u xcc=%u t0=%llu total=%llu vm=%llu bar=%llu\\n", p.tile0, (int)blockIdx.x, wave, __builtin_amdgcn_s_getreg(63492), __builtin_amdgcn_s_getreg(63508), t_start, __builtin_amdgcn_s_memtime() - t_start, sg.tvm, sg.tbar);\n') + src[j:]
+    if name in ("stamps4", "stamps5"):   # per-workgroup stamps into a device array (no printf): tools/stamps_dump.py reads it
+        src = src.replace("  int n, st, wave, lane, buf;\n", "  int n, st, wave, lane, buf;\n  unsigned long long tvm = 0, tbar = 0;\n")
+        src = src.replace("      wait_younger<NYOUNG, NBUF - 2>(k);\n    } else {\n      vm_wait<NYOUNG>();\n    }\n    lds_barrier();\n",
+                          "      const unsigned long long ta = __builtin_amdgcn_s_memtime();\n      wait_younger<NYOUNG, NBUF - 2>(k);\n"
+                          "      const unsigned long long tb = __builtin_amdgcn_s_memtime();\n      lds_barrier();\n"
+                          "      const unsigned long long tc = __builtin_amdgcn_s_memtime();\n      tvm += tb - ta; tbar += tc - tb;\n"
+                          "    } else {\n      vm_wait<NYOUNG>();\n      lds_barrier();\n    }\n")
+        src = src.replace("namespace dbsde {\n\nconstexpr int P3_WAVES = 4;",
+                          "namespace dbsde {\n\n__device__ unsigned long long g_stamps[4 * 1024 * 32];\nconstexpr int P3_WAVES = 4;")
+        for kern in ("phaseA_kernel(FusedArgs p) {\n", "phaseC_kernel(FusedArgs p) {\n"):
+            i = src.index(kern) + len(kern)
+            src = src[:i] + "  const unsigned long long t_start = __builtin_amdgcn_s_memtime();\n" + src[i:]
+        rec = ('  if ((threadIdx.x & 63) == 0) {{ unsigned long long* g = g_stamps + (({isc} + 2 * (p.tile0 != 0)) * 1024 + blockIdx.x) * 32 + wave * 8;'
+               ' g[0] = __builtin_amdgcn_s_getreg(63492); g[1] = __builtin_amdgcn_s_getreg(63508); g[2] = t_start;'
+               ' g[3] = __builtin_amdgcn_s_memtime(); g[4] = sg.tvm; g[5] = sg.tbar; g[6] = blockIdx.x; g[7] = 1; }}\n')
+        endA = src.index("// phase C: cotangents")
+        j = src.rindex("}\n", 0, endA)
+        src = src[:j] + rec.format(isc=0) + src[j:]
+        endC = src.index("}  // namespace dbsde")
+        j = src.rindex("}\n", 0, endC)
+        src = src[:j] + rec.format(isc=1) + src[j:]
+    if name == "stamps5":   # stamps4 + per-category sums: DMA issue, after() (stores / loads), MFMA regions
+        src = src.replace("  unsigned long long tvm = 0, tbar = 0;\n", "")
+        src = src.replace("  int n, st, wave, lane, buf;\n", "  int n, st, wave, lane, buf;\n  unsigned long long tvm = 0, tbar = 0, tdma = 0, taft = 0, treg = 0;\n", 1)
+        a = "    if (st + DIST < n) piece_dma(img[st + DIST], nf[st + DIST], wl + ((st + DIST) % NBUF) * buf, wave, lane);\n"
+        assert a in src
+        src = src.replace(a, "    const unsigned long long td0 = __builtin_amdgcn_s_memtime();\n" + a +
+                          "    tdma += __builtin_amdgcn_s_memtime() - td0;\n")
+        a = "    if constexpr (KB == 0) {\n      after();\n"
+        assert a in src
+        src = src.replace(a, "    if constexpr (KB == 0) {\n      const unsigned long long ta0 = __builtin_amdgcn_s_memtime();\n      after();\n"
+                          "      sg.taft += __builtin_amdgcn_s_memtime() - ta0;\n")
+        a = "    sgemm_x3_piece<TO, TI, KB + 1, PF>(acc, s, w, lane, b, sn);\n"
+        assert a in src
+        src = src.replace(a, "    const unsigned long long tr0 = __builtin_amdgcn_s_memtime();\n" + a +
+                          "    sg.treg += __builtin_amdgcn_s_memtime() - tr0;\n")
+        src = src.replace("g[6] = blockIdx.x; g[7] = 1; }", "g[6] = sg.tdma; g[7] = 1; g[8] = sg.taft; g[9] = sg.treg; }")
+        src = src.replace("* 32 + wave * 8;", "* 64 + wave * 16;")
+        src = src.replace("g_stamps[4 * 1024 * 32]", "g_stamps[4 * 1024 * 64]")
     if name in ("nostage", "bare", "bareall"):
         src = src.replace("  __device__ __forceinline__ const floatx4* next() {\n",
                           "  __device__ __forceinline__ const floatx4* next() {\n"
@@ -140,6 +179,44 @@ def build(name):
         a, b = eng_edits[name]
         assert a in e, name
         open(ep, "w").write(e.replace(a, b))
+    if name in ("stamps4", "stamps5"):   # the host-side reader of g_stamps
+        ep = os.path.join(csrc, "engine.hip")
+        e = open(ep).read()
+        e += ('\nextern "C" int dbsde_exp_stamps(unsigned long long* out, long long n) {\n'
+              '  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(dbsde::g_stamps), n * 8, 0, hipMemcpyDeviceToHost);\n}\n')
+        open(ep, "w").write(e)
+    file_edits = {   # timing-only ablations of the phase kernels' instruction classes
+        # no LDS fragment reads in the split-bf16 pieces (register constants as weights)
+        "nolds": [("phase.hpp", "w[(o + 1) & 1][p] = im[(3 * (o + 1) + p) * 64 + lane];",
+                   "w[(o + 1) & 1][p] = uintx4{(unsigned)lane, (unsigned)p, 7u, (unsigned)o};"),
+                  ("phase.hpp", "for (int p = 0; p < 3; ++p) w[0][p] = im[p * 64 + lane];",
+                   "for (int p = 0; p < 3; ++p) w[0][p] = uintx4{(unsigned)lane, (unsigned)p, 7u, 3u};"),
+                  ("phase.hpp", "for (int p = 0; p < 3; ++p) w[0][p] = im[(3 * o + p) * 64 + lane];",
+                   "for (int p = 0; p < 3; ++p) w[0][p] = uintx4{(unsigned)lane, (unsigned)p, 7u, (unsigned)o};")],
+        # no activation split: hi = x0 bits, mid = x1 bits, lo = 0 (0 VALU)
+        "nosplit": [("phase.hpp", "__device__ __forceinline__ Dw3 split_two(float x0, float x1) {",
+                     "__device__ __forceinline__ Dw3 split_two(float x0, float x1) {\n"
+                     "  if (x0 != 12345.f) return Dw3{__float_as_uint(x0), __float_as_uint(x1), 0u};")],
+        # no transcendental activation: sin -> a, cos -> 1
+        "noact": [("kernels.hpp", "__device__ __forceinline__ void fast_sincosf(float a, float& s, float& c) {",
+                   "__device__ __forceinline__ void fast_sincosf(float a, float& s, float& c) {\n"
+                   "  if (a != 12345.f) { s = a; c = 1.f; return; }")],
+        # fewer products per split-bf16 fragment (MFMA-pipe sensitivity; wrong numerics)
+        "mfma3": [("phase.hpp", "    a = mfma_bf(wc[0], s.l, a);\n    a = mfma_bf(wc[0], s.m, a);\n    a = mfma_bf(wc[1], s.m, a);\n", "")],
+        "mfma1": [("phase.hpp", "    a = mfma_bf(wc[0], s.l, a);\n    a = mfma_bf(wc[0], s.m, a);\n    a = mfma_bf(wc[1], s.m, a);\n"
+                   "    a = mfma_bf(wc[1], s.h, a);\n    a = mfma_bf(wc[2], s.h, a);\n", "")],
+        # no pinned MFMA / VALU interleave in the split-bf16 pieces
+        "nosched": [("phase.hpp", "      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA\n"
+                                  "      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU\n", "")],
+    }
+    if name in file_edits:
+        for fn, a, b in file_edits[name]:
+            fp = os.path.join(csrc, fn)
+            t = open(fp).read()
+            assert a in t, (name, a[:60])
+            open(fp, "w").write(t.replace(a, b))
+    elif name in eng_edits:
+        pass
     elif name == "stamps":    # per-piece s_memtime printf of three tiles (diagnostic build)
         defs = ["-DDBSDE_STAMPS"]
     elif name == "noslp":   # no SLP packing of f32 elementwise work into v_pk_* (MI355X_MICROARCH: anti-lever beside MFMA)
