@@ -1422,6 +1422,15 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
   return a;
 }
 
+// the split-bf16 phase kernels (T == TD) hold their piece counts at compile
+// time (phase.hpp PieceStager NP) and the piece pointers in one VGPR's lanes
+bool fused_piece_counts_ok(dbsde_ctx* c, const FusedArgs& a) {
+  const int TW = c->Wp[0] / 16, TDp = c->Dp / 16, K = c->K, hv = c->has_v ? 1 : 0;
+  if (!c->x3 || TW != TDp) return a.nA <= 64 && a.nC <= 64;
+  const int nkb = (TW + 1) / 2;
+  return a.nA == nkb * (2 + 2 * K * (1 + hv)) && a.nC == nkb * (1 + K * (2 + hv)) && a.nA <= 64 && a.nC <= 64;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -1571,6 +1580,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act, c->has_v, c->x3) : -1;
   if (fv >= 0) {
     fa = fused_args(c, R, Rp, N1, q3);
+    if (!fused_piece_counts_ok(c, fa)) return fail(c, DBSDE_EINVAL, "internal: fused kernel piece counts");
     const int nv = nv_x(c);
     const double flA = 2.0 * R * ((D + 1.0) * nv + 2.0 * K * L[1] * (double)L[1] + (double)nv * D);
     const double byA = 4.0 * R * (c->Dp + 4.0 * S + 8.0);

@@ -172,6 +172,23 @@ __device__ __forceinline__ void sgemm_piece(Mat<TO>& acc, const Mat<TI>& b, cons
 __device__ __forceinline__ void piece_dma(const float* img, int nf, floatx4* buf, int wave, int lane) {
   for (int f = wave; f < nf; f += P3_WAVES) glds16(img + (size_t)f * 256 + lane * 4, buf + f * 64);
 }
+// the same with a compile-time fragment count (split-bf16 pieces: 3 TO), unrolled
+template <int NF>
+__device__ __forceinline__ void piece_dma_n(const float* img, floatx4* buf, int wave, int lane) {
+#pragma unroll
+  for (int k = 0; k < (NF + P3_WAVES - 1) / P3_WAVES; ++k) {
+    const int f = wave + P3_WAVES * k;
+    if (k < NF / P3_WAVES || f < NF) glds16(img + (size_t)f * 256 + lane * 4, buf + f * 64);
+  }
+}
+// lane l of a VGPR pair holds piece l's image pointer (loaded once per kernel):
+// a piece's pointer is two v_readlane_b32 instead of a scalar load from the
+// kernel arguments after every barrier (the barrier's memory clobber forces
+// the reload)
+__device__ __forceinline__ const float* lane_ptr(unsigned long long v, int idx) {
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)v, idx), hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), idx);
+  return (const float*)(((unsigned long long)hi << 32) | lo);
+}
 
 // piece sequencer: wait for this piece, publish it, start the one NBUF - 1
 // ahead (NBUF-buffer LDS ring; the fp32 kernels use 2, the split-bf16 kernels,
@@ -182,17 +199,29 @@ __device__ __forceinline__ void piece_dma(const float* img, int nf, floatx4* buf
 // NBUF > 2 the DMAs of the k = min(NBUF - 2, n - 1 - st) following pieces were
 // also issued after this piece's: LC = a lower bound of this wave's chunks of
 // each (waves copy 5 or 6 of 21), so k LC more may stay in flight.
-template <int NBUF, int LC>
+//   NF > 0: every piece has NF fragments (the split-bf16 kernels) and the piece
+//   pointers come from a per-lane table (lane_ptr, n <= 64).
+//   NP > 0: the kernel's piece count at compile time (else the runtime n).
+template <int NBUF, int LC, int NF = 0, int NP = 0>
 struct PieceStagerT {
   floatx4* wl;
   const float* const* img;
   const int* nf;
   int n, st, wave, lane, buf;
+  unsigned long long ptab = 0;
   __device__ __forceinline__ void mark() {}
+  __device__ __forceinline__ void dma(int k, floatx4* dst) {
+    if constexpr (NF > 0)
+      piece_dma_n<NF>(lane_ptr(ptab, k), dst, wave, lane);
+    else
+      piece_dma(img[k], nf[k], dst, wave, lane);
+  }
+  __device__ __forceinline__ int count() const { return NP > 0 ? NP : n; }
   __device__ __forceinline__ void start() {
+    if constexpr (NF > 0) ptab = lane < count() ? (unsigned long long)img[lane] : 0ull;
 #pragma unroll
     for (int k = 0; k < NBUF - 1; ++k)
-      if (k < n) piece_dma(img[k], nf[k], wl + k * buf, wave, lane);
+      if (k < count()) dma(k, wl + k * buf);
   }
   // vm_wait<NYOUNG + LC k> for the runtime k (uniform) of younger pieces
   template <int NYOUNG, int K>
@@ -209,14 +238,14 @@ struct PieceStagerT {
   template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
     if constexpr (NBUF > 2) {
-      const int k = min(NBUF - 2, n - 1 - st);
+      const int k = min(NBUF - 2, count() - 1 - st);
       wait_younger<NYOUNG, NBUF - 2>(k);
     } else {
       vm_wait<NYOUNG>();
     }
     lds_barrier();
     constexpr int DIST = NBUF - 1;
-    if (st + DIST < n) piece_dma(img[st + DIST], nf[st + DIST], wl + ((st + DIST) % NBUF) * buf, wave, lane);
+    if (st + DIST < count()) dma(st + DIST, wl + ((st + DIST) % NBUF) * buf);
     // nothing issued later may be hoisted above the DMA (the NYOUNG counts)
     __builtin_amdgcn_sched_barrier(0);
     const floatx4* cur = wl + (st % NBUF) * buf;
@@ -225,8 +254,13 @@ struct PieceStagerT {
   }
 };
 // the kernels' stager: X3 pieces are 3 TO chunks, TO >= min(T, TD)
-template <bool X3, int T, int TD>
-using PieceStager = PieceStagerT<X3 ? P3_NBUF_X3 : 2, X3 ? (3 * (T < TD ? T : TD)) / P3_WAVES : 0>;
+// NP: pieces of phase A (PH = 0: X0, {F_j, [X_j]}, {[Z_j], B_j}, Z0) or phase C
+// (PH = 1: X0, [X_j], F_j, B_j), one per 32-wide input block in the X3 form
+template <bool X3, int T, int TD, int K = 0, bool HV = false, int PH = 0>
+using PieceStager = PieceStagerT<X3 ? P3_NBUF_X3 : 2, X3 ? (3 * (T < TD ? T : TD)) / P3_WAVES : 0, (X3 && T == TD) ? 3 * T : 0,
+                                 (X3 && T == TD && K > 0)
+                                     ? ((T + 1) / 2) * (PH == 0 ? 2 + 2 * K * (HV ? 2 : 1) : 1 + K * (HV ? 3 : 2))
+                                     : 0>;
 
 
 struct NoOp {
@@ -417,7 +451,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
   const int tile = blockIdx.x + p.tile0;   // 64-row tile (chunked launches offset it)
   const int row0 = tile * P3_ROWS + wave * 16;
   const int S = p.S, Wd = p.W;
-  PieceStager<X3, T, TD> sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
+  PieceStager<X3, T, TD, K, HV, 0> sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
   sg.start();
   Mat<TD> x;
   bload(x, p.xin, p.Dp, row0, 0);
@@ -583,7 +617,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
   const int tile = blockIdx.x + p.tile0;   // 64-row tile (chunked launches offset it)
   const int row0 = tile * P3_ROWS + wave * 16;
   const int S = p.S, Wd = p.W;
-  PieceStager<X3, T, TD> sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
+  PieceStager<X3, T, TD, K, HV, 1> sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
   sg.start();
 
   // ---- residuals and closed-form cotangents of row cl (every lane of the row
