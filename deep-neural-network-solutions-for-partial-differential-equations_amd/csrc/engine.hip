@@ -1121,7 +1121,9 @@ int prep_weights(dbsde_ctx* c, const float* params) {
 // Weight-gradient contraction, wave-owned tiles (tnw.hpp).  Problem p = j:
 // x-stack level j (alpha_j^T x + delta_j^T zbar); p = K + j: block B_j
 // (alpha_j^T h_{j-1} + delta_j^T hdot_{j-1}); plus the output-layer column sums.
-int launch_tnw(dbsde_ctx* c, int R, int Rp) {
+// Slices [s0, s0 + sn) (sn < 0: all), on stream st without profiling records
+// (st == nullptr: the context stream, profiled).
+int launch_tnw(dbsde_ctx* c, int R, int Rp, int s0 = 0, int sn = -1, hipStream_t st = nullptr) {
   const int K = c->K, S = c->Stot, T = c->Dp;
   TNWArgs a;
   memset(&a, 0, sizeof(a));
@@ -1149,6 +1151,8 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp) {
   }
   a.P = c->tnw_P;
   a.S = c->tnw_S;
+  a.s0 = s0;
+  a.sn = sn < 0 ? a.S : sn;
   a.nchunk = Rp / 16;
   a.slab = c->slabW;
   a.ubar = c->ubar;
@@ -1156,7 +1160,8 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp) {
   a.Hdk = c->Hdot + c->col[K];
   a.ldh = S;
   a.R = R;
-  if (Rp % 16 != 0 || c->Wp[K] != T || a.S % 8 != 0 || a.P != 2 * K + 2 || a.P % 4 != 0)
+  if (Rp % 16 != 0 || c->Wp[K] != T || a.S % 8 != 0 || a.P != 2 * K + 2 || a.P % 4 != 0 || a.sn % 8 != 0 ||
+      a.s0 < 0 || a.s0 + a.sn > a.S)
     return fail(c, DBSDE_EINVAL, "internal: tnw geometry");
   const double fl = 2.0 * 2.0 * (double)R * (K + 1) * c->L[1] * (c->D + 2) + 2.0 * 2.0 * (double)R * K * c->L[1] * c->L[1] +
                     4.0 * (double)R * c->L[K + 1];
@@ -1164,6 +1169,12 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp) {
   hipStream_t s = c->stream;
   (void)grid;
   if (c->tnw_nb < 1 || c->tnw_nb > 8) return fail(c, DBSDE_EINVAL, "internal: tnw tile");
+  if (st) {   // a slice range inside the phase pipeline (loss_grad_impl)
+    const int lr = c->tnw_x3 ? (Rp % 32 != 0 ? -1 : tnw_x3_launch(c->tnw_nb, a, st)) : tnw_launch(c->tnw_nb, a, st);
+    if (lr) return fail(c, DBSDE_EINVAL, "internal: tnw launch geometry");
+    HIPC(c, hipGetLastError());
+    return DBSDE_OK;
+  }
   if (c->tnw_x3) {
     if (Rp % 32 != 0) return fail(c, DBSDE_EINVAL, "internal: tnw x3 geometry");
     int lr = 0;
@@ -1576,6 +1587,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   if ((rc = join_side(c, 0))) return rc;
 
   int nloss_parts;
+  bool tnw_piped = false;
   FusedArgs fa;
   const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act, c->has_v, c->x3) : -1;
   if (fv >= 0) {
@@ -1606,6 +1618,18 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       if (c->prof) HIPC(c, hipEventRecord(c->ev_prof[0], s));
       HIPC(c, hipEventRecord(c->ev_pipe[0], s));
       const int np = std::min(c->pipes, nch);
+      // Unprofiled steps run each chunk's weight-gradient row slices on the
+      // chunk's stream right after its phase C (the slices of the first chunk
+      // overlap the second chunk's phases; slice s covers 32-row steps
+      // [s n32 / S, (s + 1) n32 / S), so the chunk boundary must be a slice
+      // boundary).  Profiled steps keep them after the section, so the section
+      // and the weight-gradient kernel are timed on their own.
+      {
+        const int S = c->tnw_S, n32 = Rp / 32, half = S / 2;
+        const long long brow = 32LL * ((long long)half * n32 / S);
+        tnw_piped = grad && c->tnw && !c->prof && nch == 2 && np == 2 && Rp % 32 == 0 && half % 8 == 0 &&
+                    brow == (long long)cu[0] * utile * P3_ROWS;
+      }
       hipStream_t ps[4] = {s, c->pipe2, c->pipe_more[0], c->pipe_more[1]};
       for (int i = 1; i < np; ++i) HIPC(c, hipStreamWaitEvent(ps[i], c->ev_pipe[0], 0));
       int t0 = 0;
@@ -1616,6 +1640,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         const int tiles = cu[i] * utile;
         kFused[fv].A<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         kFused[fv].C<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
+        if (tnw_piped && (rc = launch_tnw(c, R, Rp, i * (c->tnw_S / 2), c->tnw_S / 2, st))) return rc;
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());
@@ -1772,7 +1797,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     }
     // ---- parameter gradients
     if (c->tnw) {
-      if ((rc = launch_tnw(c, R, Rp))) return rc;
+      if (!tnw_piped && (rc = launch_tnw(c, R, Rp))) return rc;
       if ((rc = finalize_grads(c, params, grad, c->loss_part, nloss_parts, loss_dst, fo))) return rc;
     } else {
     TNArgs ta;

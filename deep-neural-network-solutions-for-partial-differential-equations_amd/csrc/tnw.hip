@@ -73,7 +73,7 @@ template <int NB>
 __global__ void __launch_bounds__(256, 1) tnw_kernel(TNWArgs a) {
   const int wg = blockIdx.x, wpg = a.P / 4;
   const int xcd = wg & 7, local = wg >> 3;
-  const int s = (local / wpg) * 8 + xcd;
+  const int s = a.s0 + (local / wpg) * 8 + xcd;
   const int p = (local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6);
   const TNWProb& pr = a.prob[p];
   const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256, 1) tnw_kernel(TNWArgs a) {
 
 template <int NB>
 static void launch_nb(const TNWArgs& a, hipStream_t s) {
-  tnw_kernel<NB><<<(unsigned)(a.S * a.P / 4), 256, 0, s>>>(a);
+  tnw_kernel<NB><<<(unsigned)(a.sn * a.P / 4), 256, 0, s>>>(a);
 }
 
 // Launch errors are left for the caller's hipGetLastError.

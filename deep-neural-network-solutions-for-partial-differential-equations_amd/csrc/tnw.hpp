@@ -38,6 +38,7 @@ struct TNWArgs {
   TNWProb prob[TNW_PMAX];
   int P;          // problems: 2K+1 weight blocks + the output layer (last)
   int S;          // row slices per problem (multiple of 8)
+  int s0, sn;     // this launch: slices [s0, s0 + sn) (sn multiple of 8; sn = S for the whole reduction)
   int nchunk;     // Rp / 16
   float* slab;    // [S][P][16NB][16NB]
   // output layer operands

@@ -132,7 +132,7 @@ template <int NB>
 __global__ void __launch_bounds__(256, 1) tnw_x3_kernel(TNWArgs a) {
   const int wg = blockIdx.x, wpg = a.P / 4;
   const int xcd = wg & 7, local = wg >> 3;
-  const int s = (local / wpg) * 8 + xcd;
+  const int s = a.s0 + (local / wpg) * 8 + xcd;
   const int p = (local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6);
   const TNWProb& pr = a.prob[p];
   const int lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(256, 1) tnw_x3_kernel(TNWArgs a) {
 
 int tnw_x3_launch(int nb, const TNWArgs& a, hipStream_t s) {
   if (nb != 7 || a.nchunk % 2 != 0) return -1;
-  tnw_x3_kernel<7><<<(unsigned)(a.S * a.P / 4), 256, 0, s>>>(a);
+  tnw_x3_kernel<7><<<(unsigned)(a.sn * a.P / 4), 256, 0, s>>>(a);
   return 0;
 }
 
