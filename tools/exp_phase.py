@@ -158,6 +158,25 @@ def build(name):
     csrc = os.path.join(tmp, "pkg", "csrc")          # csrc/../../include resolves to tmp/include
     shutil.copytree(os.path.join(PKG, "csrc"), csrc)
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
+    if name == "tnwvec":   # weight-gradient x3 operand loads as 2 float4 per lane and block (wrong layout; timing only)
+        tx = os.path.join(csrc, "tnwx3.hip")
+        t = open(tx).read()
+        a = ("  for (int j = 0; j < 8; ++j) {\n    const float* p = X + (size_t)(row0 + j) * ld + i;\n#pragma unroll\n"
+             "    for (int m = 0; m < NB; ++m) r[m][j] = p[16 * m];\n  }")
+        assert a in t, "tnwvec load_cols"
+        t = t.replace(a, "  for (int m = 0; m < NB; ++m) {\n    const float* p = X + (size_t)(row0 + (i >> 1)) * ld + 16 * m + 8 * (i & 1);\n"
+                         "    const floatx4 u = *(const floatx4*)p, v = *(const floatx4*)(p + 4);\n"
+                         "    r[m][0] = u[0]; r[m][1] = u[1]; r[m][2] = u[2]; r[m][3] = u[3];\n"
+                         "    r[m][4] = v[0]; r[m][5] = v[1]; r[m][6] = v[2]; r[m][7] = v[3];\n  }")
+        b = "    for (int j = 0; j < 8; ++j) ra[0][j] = A[(size_t)(nrow + j) * lda + i];"
+        assert b in t, "tnwvec a0"
+        t = t.replace(b, "    for (int jj = 0; jj < 1; ++jj) { const float* q4 = A + (size_t)(nrow + (i >> 1)) * lda + 8 * (i & 1); const floatx4 u = *(const floatx4*)q4, v = *(const floatx4*)(q4 + 4);"
+                         " ra[0][0] = u[0]; ra[0][1] = u[1]; ra[0][2] = u[2]; ra[0][3] = u[3]; ra[0][4] = v[0]; ra[0][5] = v[1]; ra[0][6] = v[2]; ra[0][7] = v[3]; }")
+        c = "        for (int j = 0; j < 8; ++j) ra[m + 1][j] = A[(size_t)(nrow + j) * lda + 16 * (m + 1) + i];"
+        assert c in t, "tnwvec am"
+        t = t.replace(c, "        for (int jj = 0; jj < 1; ++jj) { const float* q4 = A + (size_t)(nrow + (i >> 1)) * lda + 16 * (m + 1) + 8 * (i & 1); const floatx4 u = *(const floatx4*)q4, v = *(const floatx4*)(q4 + 4);"
+                         " ra[m + 1][0] = u[0]; ra[m + 1][1] = u[1]; ra[m + 1][2] = u[2]; ra[m + 1][3] = u[3]; ra[m + 1][4] = v[0]; ra[m + 1][5] = v[1]; ra[m + 1][6] = v[2]; ra[m + 1][7] = v[3]; }")
+        open(tx, "w").write(t)
     if name == "tnwhit":   # weight-gradient x3 operand loads from a fixed 32-row block (cache hits)
         tx = os.path.join(csrc, "tnwx3.hip")
         t = open(tx).read()
@@ -221,7 +240,7 @@ def build(name):
         defs = ["-DDBSDE_STAMPS"]
     elif name == "noslp":   # no SLP packing of f32 elementwise work into v_pk_* (MI355X_MICROARCH: anti-lever beside MFMA)
         defs = ["-fno-slp-vectorize"]
-    elif name == "tnwhit":
+    elif name in ("tnwhit", "tnwvec"):
         pass
     else:
         s2 = edit(s, name)
