@@ -27,7 +27,7 @@ EXPORTED = [
     "dbsde_abi_version", "dbsde_create", "dbsde_destroy", "dbsde_last_error", "dbsde_set_stream",
     "dbsde_param_count", "dbsde_param_used_mask", "dbsde_matrix_form", "dbsde_brownian_dim", "dbsde_set_corr", "dbsde_brownian", "dbsde_prefetch",
     "dbsde_prefetch_cancel",
-    "dbsde_loss_grad", "dbsde_net_u", "dbsde_optimizer_step", "dbsde_exact", "dbsde_hjb_mc",
+    "dbsde_loss_grad", "dbsde_net_u", "dbsde_net_u_vjp", "dbsde_optimizer_step", "dbsde_exact", "dbsde_hjb_mc",
     "dbsde_profile_enable", "dbsde_profile_count", "dbsde_profile_read", "dbsde_profile_reset",
     "dbsde_vec_reduce", "dbsde_vec_axpby", "dbsde_lbfgs_direction", "dbsde_train_step",
 ]
@@ -101,6 +101,7 @@ def load():
         "dbsde_hjb_mc": (i, [vp, vp, i, i, ctypes.c_float, ll, ctypes.c_ulonglong, vp, vp]),
         "dbsde_loss_grad": (i, [vp, vp, ctypes.POINTER(Batch), vp, ctypes.POINTER(Outputs)]),
         "dbsde_net_u": (i, [vp, vp, i, vp, vp, vp, vp]),
+        "dbsde_net_u_vjp": (i, [vp, vp, i, vp, vp, vp, vp, vp]),
         "dbsde_optimizer_step": (i, [vp, vp, vp, vp, vp, ctypes.POINTER(Optim)]),
         "dbsde_profile_enable": (i, [vp, i]),
         "dbsde_profile_count": (i, [vp]),

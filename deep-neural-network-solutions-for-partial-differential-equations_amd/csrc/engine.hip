@@ -36,7 +36,6 @@ namespace {
 
 thread_local std::string g_last_error;
 
-constexpr int TN_SPLITS_MAX = 256;  // slab capacity; the split count is chosen per context
 
 inline int pad16(int x) { return (x + 15) / 16 * 16; }
 inline int padw(int x) { return x <= 128 ? pad16(x) : (x + 127) / 128 * 128; }
@@ -750,7 +749,10 @@ int chain(dbsde_ctx* c, const char* name, ChainArgs& a, int Rp, int NP, int NT, 
   if (NP % (16 * NT) != 0) return fail(c, DBSDE_EINVAL, "internal: column tiling mismatch");
   if (a.K % CH_KC != 0) return fail(c, DBSDE_EINVAL, "internal: K not a multiple of 16");
   hipStream_t s = c->stream;
-  if (a.x3_img) {   // split-bf16 form: the weight image must hold this launch's output columns
+  // split-bf16 form (the weight image must hold this launch's output columns);
+  // tile widths without an X3 instantiation (e.g. the Z GEMM at Dp = 32) run the
+  // fp32 chain on the fp32 weights the packer writes alongside the images
+  if (a.x3_img && (NT == 7 || NT == 8)) {
     if (a.x3_tout < NP / 16 || a.x3_ti * 16 < a.K) return fail(c, DBSDE_EINVAL, "internal: x3 chain image geometry");
     switch (NT) {
       case 7:
@@ -1555,6 +1557,203 @@ int dbsde_param_used_mask(const dbsde_ctx* c, unsigned char* mask, long long n) 
 namespace {
 // dbsde_loss_grad, and dbsde_train_step's fused form (fo != NULL: the
 // optimizer update is applied inside the gradient finalize)
+// Everything after the cotangents: for the per-layer (chain) form the forward
+// tangent along zbar and the reverse, then the weight-gradient contraction and
+// the finalize (+ the fused optimizer update).  Shared by loss_grad_impl and
+// the net_u VJP.
+int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, float* grad, const double* loss_part,
+                  int nloss_parts, float* loss_dst, const FusedOpt* fo, bool tnw_piped) {
+  int rc;
+  hipStream_t s = c->stream;
+  const auto& L = c->L;
+  const int K = c->K, S = c->Stot, D = c->D;
+  if (fv < 0) {
+    // ---- forward tangent along zbar
+    {
+      ChainArgs a = base_args(c);
+      a.A = c->zbar;
+      a.lda = c->Dp;
+      a.Bt = c->BtIn;
+      x3_weights(c, a, c->imgX[0], c->Wp[0] / 16, c->Dp / 16);
+      a.ldb = c->Dp;
+      a.K = c->Dp;
+      a.in[0] = c->Abuf;
+      a.ldi[0] = S;
+      a.out[0] = c->Adot;
+      a.ldo[0] = S;
+      a.out[1] = c->Hdot;
+      a.ldo[1] = S;
+      a.lvl0_cols = c->Wp[0];
+      int nv = 0;
+      for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
+      if ((rc = chain<EPI_TAN0>(c, "gemm_xstack_tangent", a, Rp, c->Stot_x, nt_for(c->Wp[0]),
+                                2.0 * R * D * nv, 4.0 * R * (D + 2.0 * nv + L[1]))))
+        return rc;
+    }
+    for (int j = 1; j <= K; ++j) {
+      ChainArgs a = base_args(c);
+      a.A = c->Hdot + c->col[j - 1];
+      a.lda = S;
+      a.Bt = c->Bf[j];
+      x3_weights(c, a, c->imgF[j], c->Wp[j] / 16, c->Wp[j - 1] / 16);
+      a.ldb = c->Wp[j - 1];
+      a.K = c->Wp[j - 1];
+      a.in[0] = c->has_v ? c->Adot + c->col[j] : nullptr;
+      a.ldi[0] = S;
+      a.in[1] = c->Hdot + c->col[j - 1];
+      a.ldi[1] = S;
+      a.in[2] = c->Abuf + c->col[j];
+      a.ldi[2] = S;
+      a.out[0] = c->Adot + c->col[j];
+      a.ldo[0] = S;
+      a.out[1] = c->Hdot + c->col[j];
+      a.ldo[1] = S;
+      a.last = j == K;
+      a.out[2] = c->Alpha + c->col[K];
+      a.ldo[2] = S;
+      a.vec[0] = c->wout;
+      a.ubar = c->ubar;
+      if ((rc = chain<EPI_TAN>(c, "gemm_block_tangent", a, Rp, c->Wp[j], nt_for(c->Wp[j]),
+                               2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j] + 6.0 * L[j + 1]))))
+        return rc;
+    }
+    // ---- reverse over (primal, tangent)
+    for (int j = K; j >= 1; --j) {
+      ChainArgs a = base_args(c);
+      a.A = c->Alpha + c->col[j];
+      a.lda = S;
+      a.Bt = c->Bb[j];
+      x3_weights(c, a, c->imgB[j], c->Wp[j - 1] / 16, c->Wp[j] / 16);
+      a.ldb = c->Wp[j];
+      a.K = c->Wp[j];
+      a.in[0] = j == K ? nullptr : c->Pbuf[(j + 1) & 1];
+      a.ldi[0] = c->Wmax;
+      a.ubar = c->ubar;
+      a.vec[0] = c->wout;
+      a.in[1] = c->Abuf + c->col[j - 1];
+      a.ldi[1] = S;
+      a.in[2] = c->G + c->col[j - 1];
+      a.ldi[2] = S;
+      a.in[3] = c->Adot + c->col[j - 1];
+      a.ldi[3] = S;
+      a.out[0] = c->Pbuf[j & 1];
+      a.ldo[0] = c->Wmax;
+      a.out[1] = c->Alpha + c->col[j - 1];
+      a.ldo[1] = S;
+      if ((rc = chain<EPI_REV>(c, "gemm_block_reverse", a, Rp, c->Wp[j - 1], nt_for(c->Wp[j - 1]),
+                               2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j + 1] + 6.0 * L[j]))))
+        return rc;
+    }
+  }
+  // ---- parameter gradients
+  if (c->tnw) {
+    if (!tnw_piped && (rc = launch_tnw(c, R, Rp))) return rc;
+    if ((rc = finalize_grads(c, params, grad, loss_part, nloss_parts, loss_dst, fo))) return rc;
+  } else {
+  TNArgs ta;
+  memset(&ta, 0, sizeof(ta));
+  const int S_ = c->tn_splits;
+  const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
+  ta.rows_per_split = rps;
+  ta.Rp = Rp;
+  double tfl = 0.0;
+  {
+    TNProb& p0 = ta.prob[0];
+    p0.A[0] = c->Alpha;
+    p0.lda[0] = S;
+    p0.nA[0] = c->Stot_x;
+    p0.B[0] = c->xin;
+    p0.ldb[0] = c->Dp;
+    p0.nB[0] = c->Dp;
+    p0.A[1] = c->Delta;
+    p0.lda[1] = S;
+    p0.nA[1] = c->Stot_x;
+    p0.B[1] = c->zbar;
+    p0.ldb[1] = c->Dp;
+    p0.nB[1] = c->Dp;
+    p0.npairs = 2;
+    p0.ones_col = -1;
+    p0.mv = c->slab_mv[0];
+    p0.nv = c->slab_nv[0];
+    p0.mt = c->slab_mt[0];
+    p0.nt = c->slab_nt[0];
+    p0.slab = c->slab[0];
+    int nv = 0;
+    for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
+    tfl += 2.0 * 2.0 * R * nv * (D + 2);
+  }
+  int maxt = ta.prob[0].mt * ta.prob[0].nt;
+  for (int j = 1; j <= K; ++j) {
+    TNProb& pj = ta.prob[j];
+    pj.A[0] = c->Alpha + c->col[j];
+    pj.lda[0] = S;
+    pj.nA[0] = c->Wp[j];
+    pj.B[0] = c->H + c->col[j - 1];
+    pj.ldb[0] = S;
+    pj.nB[0] = c->Wp[j - 1];
+    pj.A[1] = c->Delta + c->col[j];
+    pj.lda[1] = S;
+    pj.nA[1] = c->Wp[j];
+    pj.B[1] = c->Hdot + c->col[j - 1];
+    pj.ldb[1] = S;
+    pj.nB[1] = c->Wp[j - 1];
+    pj.npairs = 2;
+    pj.ones_col = c->has_v ? -1 : c->Wp[j - 1];
+    pj.mv = c->slab_mv[j];
+    pj.nv = c->slab_nv[j];
+    pj.mt = c->slab_mt[j];
+    pj.nt = c->slab_nt[j];
+    pj.slab = c->slab[j];
+    maxt = std::max(maxt, pj.mt * pj.nt);
+    tfl += 2.0 * 2.0 * R * L[j] * (L[j + 1] + (c->has_v ? 0 : 1));
+  }
+  {
+    // output layer: [w_out | b_out] = sum_r ubar_r [h_{K+1} | 1] + hdot_{K+1}
+    TNProb& po = ta.prob[K + 1];
+    po.A[0] = c->u16;
+    po.lda[0] = 16;
+    po.nA[0] = 16;
+    po.B[0] = c->H + c->col[K];
+    po.ldb[0] = S;
+    po.nB[0] = c->Wp[K];
+    po.A[1] = c->o16;
+    po.lda[1] = 16;
+    po.nA[1] = 16;
+    po.B[1] = c->Hdot + c->col[K];
+    po.ldb[1] = S;
+    po.nB[1] = c->Wp[K];
+    po.npairs = 2;
+    po.ones_col = c->Wp[K];
+    po.mv = 1;
+    po.nv = c->slab_nv[K + 1];
+    po.mt = c->slab_mt[K + 1];
+    po.nt = c->slab_nt[K + 1];
+    po.slab = c->slab[K + 1];
+    maxt = std::max(maxt, po.mt * po.nt);
+    tfl += 2.0 * 2.0 * R * (L[K + 1] + 1);
+  }
+  if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
+  if (c->x3chain) {
+    // split-bf16 tiles for the layer problems (tnx3.hpp), the fp32 kernel
+    // for the one-row output layer
+    int maxt3 = 0;
+    for (int j = 0; j <= K; ++j)
+      maxt3 = std::max(maxt3, ((ta.prob[j].nA[0] + TX_TILE - 1) / TX_TILE) * ((ta.prob[j].nB[0] + TX_TILE - 1) / TX_TILE));
+    const int rps32 = ((Rp + S_ - 1) / S_ + 31) / 32 * 32;
+    if (Rp % 32 != 0) return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
+    TNArgs to = ta;
+    to.prob[0] = ta.prob[K + 1];
+    RUN(c, "tn_weight_grad", tfl, 0.0,
+        tn_x3_kernel<<<dim3(maxt3, (Rp + rps32 - 1) / rps32, K + 1), 256, 0, s>>>(ta, rps32);
+        tn_gemm_kernel<<<dim3(ta.prob[K + 1].mt * ta.prob[K + 1].nt, S_, 1), 256, 0, s>>>(to));
+  } else {
+    RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
+  }
+  if ((rc = finalize_grads(c, params, grad, nullptr, 0, nullptr, fo))) return rc;
+  }
+  return DBSDE_OK;
+}
+
 int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, float* grad, const dbsde_outputs* out,
                    const FusedOpt* fo) {
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
@@ -1716,192 +1915,8 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
        })))
     return rc;
 
-  if (grad) {
-    if (fv < 0) {
-      // ---- forward tangent along zbar
-      {
-        ChainArgs a = base_args(c);
-        a.A = c->zbar;
-        a.lda = c->Dp;
-        a.Bt = c->BtIn;
-        x3_weights(c, a, c->imgX[0], c->Wp[0] / 16, c->Dp / 16);
-        a.ldb = c->Dp;
-        a.K = c->Dp;
-        a.in[0] = c->Abuf;
-        a.ldi[0] = S;
-        a.out[0] = c->Adot;
-        a.ldo[0] = S;
-        a.out[1] = c->Hdot;
-        a.ldo[1] = S;
-        a.lvl0_cols = c->Wp[0];
-        int nv = 0;
-        for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
-        if ((rc = chain<EPI_TAN0>(c, "gemm_xstack_tangent", a, Rp, c->Stot_x, nt_for(c->Wp[0]),
-                                  2.0 * R * D * nv, 4.0 * R * (D + 2.0 * nv + L[1]))))
-          return rc;
-      }
-      for (int j = 1; j <= K; ++j) {
-        ChainArgs a = base_args(c);
-        a.A = c->Hdot + c->col[j - 1];
-        a.lda = S;
-        a.Bt = c->Bf[j];
-        x3_weights(c, a, c->imgF[j], c->Wp[j] / 16, c->Wp[j - 1] / 16);
-        a.ldb = c->Wp[j - 1];
-        a.K = c->Wp[j - 1];
-        a.in[0] = c->has_v ? c->Adot + c->col[j] : nullptr;
-        a.ldi[0] = S;
-        a.in[1] = c->Hdot + c->col[j - 1];
-        a.ldi[1] = S;
-        a.in[2] = c->Abuf + c->col[j];
-        a.ldi[2] = S;
-        a.out[0] = c->Adot + c->col[j];
-        a.ldo[0] = S;
-        a.out[1] = c->Hdot + c->col[j];
-        a.ldo[1] = S;
-        a.last = j == K;
-        a.out[2] = c->Alpha + c->col[K];
-        a.ldo[2] = S;
-        a.vec[0] = c->wout;
-        a.ubar = c->ubar;
-        if ((rc = chain<EPI_TAN>(c, "gemm_block_tangent", a, Rp, c->Wp[j], nt_for(c->Wp[j]),
-                                 2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j] + 6.0 * L[j + 1]))))
-          return rc;
-      }
-      // ---- reverse over (primal, tangent)
-      for (int j = K; j >= 1; --j) {
-        ChainArgs a = base_args(c);
-        a.A = c->Alpha + c->col[j];
-        a.lda = S;
-        a.Bt = c->Bb[j];
-        x3_weights(c, a, c->imgB[j], c->Wp[j - 1] / 16, c->Wp[j] / 16);
-        a.ldb = c->Wp[j];
-        a.K = c->Wp[j];
-        a.in[0] = j == K ? nullptr : c->Pbuf[(j + 1) & 1];
-        a.ldi[0] = c->Wmax;
-        a.ubar = c->ubar;
-        a.vec[0] = c->wout;
-        a.in[1] = c->Abuf + c->col[j - 1];
-        a.ldi[1] = S;
-        a.in[2] = c->G + c->col[j - 1];
-        a.ldi[2] = S;
-        a.in[3] = c->Adot + c->col[j - 1];
-        a.ldi[3] = S;
-        a.out[0] = c->Pbuf[j & 1];
-        a.ldo[0] = c->Wmax;
-        a.out[1] = c->Alpha + c->col[j - 1];
-        a.ldo[1] = S;
-        if ((rc = chain<EPI_REV>(c, "gemm_block_reverse", a, Rp, c->Wp[j - 1], nt_for(c->Wp[j - 1]),
-                                 2.0 * R * L[j] * L[j + 1], 4.0 * R * (L[j + 1] + 6.0 * L[j]))))
-          return rc;
-      }
-    }
-    // ---- parameter gradients
-    if (c->tnw) {
-      if (!tnw_piped && (rc = launch_tnw(c, R, Rp))) return rc;
-      if ((rc = finalize_grads(c, params, grad, c->loss_part, nloss_parts, loss_dst, fo))) return rc;
-    } else {
-    TNArgs ta;
-    memset(&ta, 0, sizeof(ta));
-    const int S_ = c->tn_splits;
-    const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
-    ta.rows_per_split = rps;
-    ta.Rp = Rp;
-    double tfl = 0.0;
-    {
-      TNProb& p0 = ta.prob[0];
-      p0.A[0] = c->Alpha;
-      p0.lda[0] = S;
-      p0.nA[0] = c->Stot_x;
-      p0.B[0] = c->xin;
-      p0.ldb[0] = c->Dp;
-      p0.nB[0] = c->Dp;
-      p0.A[1] = c->Delta;
-      p0.lda[1] = S;
-      p0.nA[1] = c->Stot_x;
-      p0.B[1] = c->zbar;
-      p0.ldb[1] = c->Dp;
-      p0.nB[1] = c->Dp;
-      p0.npairs = 2;
-      p0.ones_col = -1;
-      p0.mv = c->slab_mv[0];
-      p0.nv = c->slab_nv[0];
-      p0.mt = c->slab_mt[0];
-      p0.nt = c->slab_nt[0];
-      p0.slab = c->slab[0];
-      int nv = 0;
-      for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
-      tfl += 2.0 * 2.0 * R * nv * (D + 2);
-    }
-    int maxt = ta.prob[0].mt * ta.prob[0].nt;
-    for (int j = 1; j <= K; ++j) {
-      TNProb& pj = ta.prob[j];
-      pj.A[0] = c->Alpha + c->col[j];
-      pj.lda[0] = S;
-      pj.nA[0] = c->Wp[j];
-      pj.B[0] = c->H + c->col[j - 1];
-      pj.ldb[0] = S;
-      pj.nB[0] = c->Wp[j - 1];
-      pj.A[1] = c->Delta + c->col[j];
-      pj.lda[1] = S;
-      pj.nA[1] = c->Wp[j];
-      pj.B[1] = c->Hdot + c->col[j - 1];
-      pj.ldb[1] = S;
-      pj.nB[1] = c->Wp[j - 1];
-      pj.npairs = 2;
-      pj.ones_col = c->has_v ? -1 : c->Wp[j - 1];
-      pj.mv = c->slab_mv[j];
-      pj.nv = c->slab_nv[j];
-      pj.mt = c->slab_mt[j];
-      pj.nt = c->slab_nt[j];
-      pj.slab = c->slab[j];
-      maxt = std::max(maxt, pj.mt * pj.nt);
-      tfl += 2.0 * 2.0 * R * L[j] * (L[j + 1] + (c->has_v ? 0 : 1));
-    }
-    {
-      // output layer: [w_out | b_out] = sum_r ubar_r [h_{K+1} | 1] + hdot_{K+1}
-      TNProb& po = ta.prob[K + 1];
-      po.A[0] = c->u16;
-      po.lda[0] = 16;
-      po.nA[0] = 16;
-      po.B[0] = c->H + c->col[K];
-      po.ldb[0] = S;
-      po.nB[0] = c->Wp[K];
-      po.A[1] = c->o16;
-      po.lda[1] = 16;
-      po.nA[1] = 16;
-      po.B[1] = c->Hdot + c->col[K];
-      po.ldb[1] = S;
-      po.nB[1] = c->Wp[K];
-      po.npairs = 2;
-      po.ones_col = c->Wp[K];
-      po.mv = 1;
-      po.nv = c->slab_nv[K + 1];
-      po.mt = c->slab_mt[K + 1];
-      po.nt = c->slab_nt[K + 1];
-      po.slab = c->slab[K + 1];
-      maxt = std::max(maxt, po.mt * po.nt);
-      tfl += 2.0 * 2.0 * R * (L[K + 1] + 1);
-    }
-    if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
-    if (c->x3chain) {
-      // split-bf16 tiles for the layer problems (tnx3.hpp), the fp32 kernel
-      // for the one-row output layer
-      int maxt3 = 0;
-      for (int j = 0; j <= K; ++j)
-        maxt3 = std::max(maxt3, ((ta.prob[j].nA[0] + TX_TILE - 1) / TX_TILE) * ((ta.prob[j].nB[0] + TX_TILE - 1) / TX_TILE));
-      const int rps32 = ((Rp + S_ - 1) / S_ + 31) / 32 * 32;
-      if (Rp % 32 != 0) return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
-      TNArgs to = ta;
-      to.prob[0] = ta.prob[K + 1];
-      RUN(c, "tn_weight_grad", tfl, 0.0,
-          tn_x3_kernel<<<dim3(maxt3, (Rp + rps32 - 1) / rps32, K + 1), 256, 0, s>>>(ta, rps32);
-          tn_gemm_kernel<<<dim3(ta.prob[K + 1].mt * ta.prob[K + 1].nt, S_, 1), 256, 0, s>>>(to));
-    } else {
-      RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
-    }
-    if ((rc = finalize_grads(c, params, grad, nullptr, 0, nullptr, fo))) return rc;
-    }
-  }
+  if (grad && (rc = backward_tail(c, params, R, Rp, fv, grad, c->loss_part, nloss_parts, loss_dst, fo, tnw_piped)))
+    return rc;
 
   if (out && (out->X || out->Y || out->Z)) {
     const long long n = (long long)R * D;
@@ -2020,6 +2035,49 @@ int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const 
       export_kernel<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, nullptr, u,
                                                                 Du));
   return DBSDE_OK;
+}
+
+// net_u's VJP (loss.backward through the reference's net_u outputs,
+// nd_BSPDE_case.py:191-221 with create_graph=True): grad = d/dparams of
+// sum_r ubar_r u_r + zbar_r . Du_r at the points (t, X).  The same backward as
+// dbsde_loss_grad with the caller's cotangents in place of the BSDE residual
+// ones: the fused phase kernels take them in phase C's prologue, the per-layer
+// form in its ubar / zbar buffers.
+int dbsde_net_u_vjp(dbsde_ctx* c, const float* params, int R, const float* t, const float* X, const float* ubar,
+                    const float* zbar, float* grad) {
+  if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
+  if (!params || !t || !X || !ubar || !zbar || !grad || R < 1) return fail(c, DBSDE_EINVAL, "bad net_u_vjp arguments");
+  HIPC(c, hipSetDevice(c->device));
+  const int Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD, D = c->D;
+  int rc;
+  if ((rc = ensure_rows(c, Rp, 1))) return rc;
+  hipStream_t s = c->stream;
+  if ((rc = prep_weights(c, params))) return rc;
+  bool from_pf;
+  if ((rc = select_paths(c, nullptr, from_pf))) return rc;
+  const long long n = (long long)Rp * c->Dp;
+  const unsigned nb = (unsigned)((n + 255) / 256);
+  RUN(c, "netu_input", 0.0, 0.0, netu_input_kernel<<<nb, 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
+  if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
+  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3) : -1;
+  if (fv >= 0) {
+    // ubar -> rres rows, zbar -> the sdw rows phase C reads (phase A's use of
+    // sdw only feeds the residual row sums, unused here)
+    RUN(c, "vjp_cotangents", 0.0, 0.0,
+        ext_cotan_kernel<<<nb, 256, 0, s>>>(ubar, zbar, R, Rp, D, c->Dp, nullptr, c->rres, c->sdw, nullptr));
+    FusedArgs fa = fused_args(c, R, Rp, 1, false);
+    if (!fused_piece_counts_ok(c, fa)) return fail(c, DBSDE_EINVAL, "internal: fused kernel piece counts");
+    fa.cp.ext = 1;
+    fa.cp.ext_ub = c->rres;
+    RUN(c, "fused_fwd_inputgrad", 0.0, 0.0, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+    RUN(c, "fused_tangent_reverse", 0.0, 0.0, kFused[fv].C<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+  } else {
+    if ((rc = forward_and_inputgrad(c, R, Rp, false))) return rc;
+    RUN(c, "vjp_cotangents", 0.0, 0.0,
+        ext_cotan_kernel<<<nb, 256, 0, s>>>(ubar, zbar, R, Rp, D, c->Dp, c->u_clamp ? c->umask : nullptr, c->ubar,
+                                            c->zbar, c->u16));
+  }
+  return backward_tail(c, params, R, Rp, fv, grad, nullptr, 0, nullptr, nullptr, false);
 }
 
 int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, float* v, const dbsde_optim* o) {

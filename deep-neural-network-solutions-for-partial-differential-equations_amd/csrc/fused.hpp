@@ -20,6 +20,10 @@ struct CotanParams {
   const float* q3S;         // [N] or null
   float phi_r, phi_c, phi_zz, strike, g_alpha;
   int g_kind;
+  // net_u VJP (dbsde_net_u_vjp): caller cotangents instead of the BSDE
+  // residual ones -- ubar from ext_ub [Rp], zbar from the sdw rows
+  int ext;
+  const float* ext_ub;
 };
 
 struct FusedArgs {

@@ -450,6 +450,27 @@ __global__ void __launch_bounds__(256) ubar_kernel(const float* rres, const floa
   if (threadIdx.x == 0) loss_part[blockIdx.x] = red[0];
 }
 
+// net_u VJP inputs (dbsde_net_u_vjp): the caller's ubar [R] and zbar [R, D]
+// as row buffers -- ub [Rp] (zero past R) and z rows [Rp, ldz] (columns
+// 1..D, zero elsewhere).  With umask (the per-layer form, Heston u-clamp) the
+// values are masked here and u16 (the output-layer operand) is written too.
+__global__ void __launch_bounds__(256) ext_cotan_kernel(const float* ubar, const float* zbar, int R, int Rp, int D,
+                                                        int ldz, const float* umask, float* ub, float* zrows,
+                                                        float* u16) {
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i < (long long)Rp * ldz) {
+    const int r = (int)(i / ldz), col = (int)(i - (long long)r * ldz);
+    const float m = (umask && r < R) ? umask[r] : 1.f;
+    zrows[i] = (r < R && col >= 1 && col <= D) ? m * zbar[(size_t)r * D + col - 1] : 0.f;
+  }
+  if (i < Rp) {
+    const float m = (umask && i < R) ? umask[i] : 1.f;
+    const float v = i < R ? m * ubar[i] : 0.f;
+    ub[i] = v;
+    if (u16) u16[(size_t)i * 16] = v;
+  }
+}
+
 __global__ void __launch_bounds__(256) loss_final_kernel(const double* part, int n, float* loss) {
   __shared__ double red[256];
   double a = 0.0;

@@ -624,7 +624,11 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
   // computes them; the zbar columns 16 o + 4 q + r are this lane's)
   const CotanParams& cp = p.cp;
   const int r = row0 + cl;
-  const RowCotan rc = row_cotan(cp, r);
+  RowCotan rc = row_cotan(cp, r);
+  if (cp.ext) {   // net_u VJP: the caller's (ubar, zbar), through the u-clamp mask
+    rc.ub = rc.valid ? rc.mask * cp.ext_ub[r] : 0.f;
+    rc.res = 0.f;
+  }
   Mat<TD> zb;
   float tz = 0.f;
   {
@@ -644,8 +648,9 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int c = 16 * o + 4 * q + rr;
-        zb.v[o][rr] = (rc.valid && c >= 1 && c <= p.D) ? col_zbar(cp, rc, c, xv.v[o][rr], zv.v[o][rr], sv.v[o][rr], tz)
-                                                       : 0.f;
+        zb.v[o][rr] = (rc.valid && c >= 1 && c <= p.D)
+                          ? (cp.ext ? rc.mask * sv.v[o][rr] : col_zbar(cp, rc, c, xv.v[o][rr], zv.v[o][rr], sv.v[o][rr], tz))
+                          : 0.f;
       }
   }
   bstore_stream(zb, p.zbar, p.Dp, row0, 0);

@@ -58,6 +58,33 @@ def _world():
     return 0, 1
 
 
+class _NetU(torch.autograd.Function):
+    """FBSNN.net_u as a differentiable op: forward dbsde_net_u, backward the
+    native VJP dbsde_net_u_vjp (parameter gradients of sum ubar u + zbar . Du),
+    split into the model parameters."""
+
+    @staticmethod
+    def forward(ctx, fb, t, X, *params):
+        u = torch.empty((X.shape[0], 1), device=X.device)
+        du = torch.empty_like(X)
+        fb.solver.net_u(fb.params, t, X, u, du)
+        ctx.fb = fb
+        ctx.save_for_backward(t, X)
+        return u, du
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gu, gdu):
+        fb = ctx.fb
+        t, X = ctx.saved_tensors
+        gu = torch.zeros(X.shape[0], device=X.device) if gu is None else gu.reshape(-1).float().contiguous()
+        gdu = torch.zeros_like(X) if gdu is None else gdu.float().contiguous()
+        g = torch.empty_like(fb.params)
+        fb.solver.net_u_vjp(fb.params, t, X, gu, gdu, g)
+        grads = tuple(g[o:o + n].view(shape) for o, n, shape in fb._param_slices())
+        return (None, None, None) + grads
+
+
 class FBSNN(ABC):
     """nd_BSPDE_case.py:126 / with_corr_high_dimension_pde.py:132 surface."""
 
@@ -212,16 +239,35 @@ class FBSNN(ABC):
         return out
 
     def net_u(self, t, X):
-        """DeepBSDE.py:189-194: (u [R,1], Du [R,D]) at the given points."""
+        """DeepBSDE.py:189-194: (u [R,1], Du [R,D]) at the given points.  With
+        grad mode on, (u, Du) are connected to the model parameters as in the
+        reference (nd_BSPDE_case.py:191-221, create_graph=True): a backward
+        through them runs the native VJP (dbsde_net_u_vjp) and accumulates
+        into each parameter's .grad.  The points are not differentiated."""
         X = torch.as_tensor(X, dtype=torch.float32).to(self.device)
         if X.dim() == 1:
             X = X.unsqueeze(-1)
         t = torch.as_tensor(t, dtype=torch.float32).to(self.device).reshape(-1).contiguous()
-        X = X.reshape(-1, self.state_dim).contiguous()
+        X = X.detach().reshape(-1, self.state_dim).contiguous()
+        params = [p for _, p in self.model.named_parameters()]
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _NetU.apply(self, t, X, *params)
         u = torch.empty((X.shape[0], 1), device=self.device)
         du = torch.empty_like(X)
         self.solver.net_u(self.params, t, X, u, du)
         return u, du
+
+    def _param_slices(self):
+        """(offset, numel, shape) of every model parameter in the flat vector, in
+        named_parameters() order (the flat vector is in state_dict order,
+        networks.bind)."""
+        if getattr(self, "_pslices", None) is None:
+            off, where = 0, {}
+            for name, p in self.model.state_dict().items():
+                where[name] = (off, p.numel(), p.shape)
+                off += p.numel()
+            self._pslices = [where[name] for name, _ in self.model.named_parameters()]
+        return self._pslices
 
     def Dg_tf(self, X):
         """DeepBSDE.py:196-200 (torch autograd of the problem's g_tf)."""

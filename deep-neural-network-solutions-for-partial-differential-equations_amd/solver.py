@@ -182,6 +182,17 @@ class NativeSolver:
         _lib.check(self.lib.dbsde_net_u(self.ctx, _ptr(params), R, _ptr(t), _ptr(X), _ptr(u), _ptr(Du)),
                    self.ctx)
 
+    def net_u_vjp(self, params, t, X, ubar, zbar, grad):
+        """grad <- d/dparams [sum ubar u + sum zbar . Du] at (t, X) (dbsde_net_u_vjp)."""
+        R = X.numel() // self.D
+        self._check_tensor(params, "params", self.nparams)
+        for name, v, n in (("t", t, R), ("X", X, R * self.D), ("ubar", ubar, R), ("zbar", zbar, R * self.D),
+                           ("grad", grad, self.nparams)):
+            self._check_tensor(v, name, n)
+        self._bind_stream()
+        _lib.check(self.lib.dbsde_net_u_vjp(self.ctx, _ptr(params), R, _ptr(t), _ptr(X), _ptr(ubar), _ptr(zbar),
+                                            _ptr(grad)), self.ctx)
+
     def optimizer_step(self, params, grad, m, v, **opt):
         """clip_grad_norm_ + optimizer.step() over the flat parameters; m, v are
         the optimizer's state buffers (see include/dbsde.h DBSDE_OPT_*); opt as

@@ -215,6 +215,15 @@ int dbsde_loss_grad(dbsde_ctx* ctx, const float* params, const dbsde_batch* batc
 int dbsde_net_u(dbsde_ctx* ctx, const float* params, int R, const float* t,
                 const float* X, float* u, float* Du);
 
+/* The vector-Jacobian product of net_u: the gradient the reference's autograd
+ * graph of (u, Du) delivers (nd_BSPDE_case.py:191-221, create_graph=True),
+ *   grad = d/dparams [ sum_r ubar[r] u[r] + sum_{r,d} zbar[r,d] Du[r,d] ]
+ * at the R points (t [R], X [R,D]); ubar [R], zbar [R,D], grad (flat,
+ * param_count) are device buffers (grad overwritten).  Not the gradient with
+ * respect to X. */
+int dbsde_net_u_vjp(dbsde_ctx* ctx, const float* params, int R, const float* t,
+                    const float* X, const float* ubar, const float* zbar, float* grad);
+
 /* optimizers (nd_BSPDE_case.py:331-350), torch.optim single-tensor formula order */
 #define DBSDE_OPT_ADAM 0
 #define DBSDE_OPT_ADAMW 1
