@@ -305,7 +305,8 @@ def main():
 
     def sym_of(rec):
         if form & 2 and rec in KERNEL_SYMBOL_X3:
-            return KERNEL_SYMBOL_X3[rec]
+            # the chain layouts' split-bf16 weight-gradient tiles (tnx3.hpp)
+            return "tn_x3_kernel" if (form & 4 and rec == "tn_weight_grad") else KERNEL_SYMBOL_X3[rec]
         return KERNEL_SYMBOL.get(rec, rec)
 
     avg_ms = st["ms"] / st["launches"]

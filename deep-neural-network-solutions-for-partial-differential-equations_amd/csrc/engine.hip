@@ -1455,7 +1455,10 @@ int dbsde_abi_version(void) { return DBSDE_ABI_VERSION; }
 
 int dbsde_matrix_form(const dbsde_ctx* c) {
   if (!c) return 0;
-  return (c->x3 ? 1 : 0) | (c->tnw && c->tnw_x3 ? 2 : 0) | (c->x3chain ? 4 : 0);
+  // bit 1: the wave-tile weight-gradient kernel in split-bf16 form, or the
+  // chain layouts' weight-gradient tiles (tnx3.hpp, split-bf16 with x3chain)
+  const bool tn_x3 = c->tnw ? c->tnw_x3 : c->x3chain;
+  return (c->x3 ? 1 : 0) | (tn_x3 ? 2 : 0) | (c->x3chain ? 4 : 0);
 }
 
 const char* dbsde_last_error(const dbsde_ctx* ctx) {

@@ -123,7 +123,8 @@ int dbsde_param_used_mask(const dbsde_ctx* ctx, unsigned char* mask, long long n
 
 /* matrix-core form of this network's kernels (no reference counterpart:
  * reporting only).  Bit 0: the fused phase kernels, bit 1: the weight-gradient
- * kernel, bit 2: the per-layer chain GEMMs (FC / Resnet layouts without a
+ * kernel (wave-owned tiles, or the chain layouts' 128x128 tiles), bit 2: the
+ * per-layer chain GEMMs (FC / Resnet layouts without a
  * fused variant) run fp32 operands as exact split-bf16 triples (six bf16 MFMAs
  * per product block, fp32 accumulation, error at or below the fp32-input
  * MFMA's); 0 = fp32-input MFMA (v_mfma_f32_16x16x4_f32) throughout.  Set at

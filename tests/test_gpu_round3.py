@@ -362,3 +362,30 @@ def test_fused_update_equals_separate_optimizer(pkg, dev, name):
     for x, y in ((a.params, b.params), (oa["m"], ob["m"]), (oa["v"], ob["v"])):   # (ASGD diverges to NaN here)
         torch.testing.assert_close(x, y, rtol=0, atol=0, equal_nan=True)
     assert a.optimizer_steps_taken(oa) == b.optimizer_steps_taken(ob) == 3
+
+
+# --------------------------------------------------------------------------- chain form at small D
+def test_fc256_small_dim_chain_matches_oracle(pkg, dev):
+    """FC-Sine [21, 256x4, 1] (config 4's network at D = 20): the per-layer
+    split-bf16 chain, whose Z GEMM (Dp = 32, two 16-column tiles) has no
+    split-bf16 instantiation and runs the fp32 chain on the packer's fp32
+    weights.  Loss / Y / Z / gradient against the oracle's autograd
+    (hjb_implement.py:590-604 problem, M = 16, N = 5)."""
+    torch.manual_seed(21)
+    D, M, N = 20, 16, 5
+    layers = [D + 1] + 4 * [256] + [1]
+    model = fr.build_model("FC", layers, "Sine")
+    params = fr.flat_params(model)
+    np.random.seed(22)
+    t, W = fr.fetch_minibatch(M, N, D, 1.0)
+    Xi = np.zeros((1, D))
+    torch.set_num_threads(4)
+    ref = fr.loss_and_grads(model, fr.make_problem("hjb", D), t, W, torch.from_numpy(Xi).float(), M, D)
+    spec = pkg.ProblemSpec(sig_b=float(np.sqrt(2.0)), phi_zz=1.0, g="log")
+    s = pkg.NativeSolver("FC", layers, "Sine", spec, 1.0, dev)
+    assert s.matrix_form & 4, "expected the split-bf16 chain form"
+    r = _native(s, torch.from_numpy(params).to(dev), M, N, D, Xi, t.squeeze(-1), W, dev)
+    np.testing.assert_allclose(r["loss"][0], ref["loss"], rtol=1e-4)
+    np.testing.assert_allclose(r["Y"], ref["Y"], rtol=0, atol=1e-4 * max(1.0, np.abs(ref["Y"]).max()))
+    np.testing.assert_allclose(r["Z"], ref["Z"], rtol=0, atol=1e-4 * max(1.0, np.abs(ref["Z"]).max()))
+    np.testing.assert_allclose(r["grad"], ref["grad"], rtol=0, atol=2e-4 * np.abs(ref["grad"]).max())
