@@ -1826,11 +1826,13 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       // [s n32 / S, (s + 1) n32 / S), so the chunk boundary must be a slice
       // boundary).  Profiled steps keep them after the section, so the section
       // and the weight-gradient kernel are timed on their own.
+      int sb = 0;   // first slice of chunk 1
       {
-        const int S = c->tnw_S, n32 = Rp / 32, half = S / 2;
-        const long long brow = 32LL * ((long long)half * n32 / S);
-        tnw_piped = grad && c->tnw && !c->prof && nch == 2 && np == 2 && Rp % 32 == 0 && half % 8 == 0 &&
-                    brow == (long long)cu[0] * utile * P3_ROWS;
+        const int S = c->tnw_S, n32 = Rp / 32;
+        const long long crow = (long long)cu[0] * utile * P3_ROWS;
+        for (int k = 8; k < S && !sb; k += 8)
+          if (32LL * ((long long)k * n32 / S) == crow) sb = k;
+        tnw_piped = grad && c->tnw && !c->prof && nch == 2 && np == 2 && Rp % 32 == 0 && sb > 0;
       }
       hipStream_t ps[4] = {s, c->pipe2, c->pipe_more[0], c->pipe_more[1]};
       for (int i = 1; i < np; ++i) HIPC(c, hipStreamWaitEvent(ps[i], c->ev_pipe[0], 0));
@@ -1842,7 +1844,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         const int tiles = cu[i] * utile;
         kFused[fv].A<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         kFused[fv].C<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
-        if (tnw_piped && (rc = launch_tnw(c, R, Rp, i * (c->tnw_S / 2), c->tnw_S / 2, st))) return rc;
+        if (tnw_piped && (rc = launch_tnw(c, R, Rp, i == 0 ? 0 : sb, i == 0 ? sb : c->tnw_S - sb, st))) return rc;
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());

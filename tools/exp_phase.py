@@ -191,6 +191,11 @@ def build(name):
     eng_edits = {   # engine.hip launch-shape variants
         "onechunk": ("  int chunks = 2;", "  int chunks = 1;"),    # all of phase A, then all of phase C
         "onepipe": ("  int pipes = 2;", "  int pipes = 1;"),       # A0 C0 A1 C1 in order on one stream
+        # unequal path chunks (units of 64 paths; 16 at the north star)
+        "c0_6": ("  int chunk0 = 0;", "  int chunk0 = 6;"),
+        "c0_7": ("  int chunk0 = 0;", "  int chunk0 = 7;"),
+        "c0_9": ("  int chunk0 = 0;", "  int chunk0 = 9;"),
+        "c0_10": ("  int chunk0 = 0;", "  int chunk0 = 10;"),
     }
     if name in eng_edits:
         ep = os.path.join(csrc, "engine.hip")
