@@ -858,6 +858,7 @@ int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
     const int nthr = ra.M * ra.nb;
     RUN(c, name, 0.0, bytes, rollout_heston_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
   } else if (c->Lt && !ra.W) {
+    if (ra.ldx > CP_SROW) return fail(c, DBSDE_EINVAL, "internal: correlated rollout row staging");
     RUN(c, name, 2.0 * steps * ra.nb * ra.nb / 2, bytes,
         launch_corr(ra, s));
   } else {

@@ -186,6 +186,13 @@ constexpr int CP_PATHS = 16;
 constexpr int CP_TS = 36;
 constexpr int CP_BUF = 4 * 4 * CP_PATHS * CP_TS;   // floats per 4-step buffer
 constexpr int CP_THREADS = 512;                     // 8 waves: one per output block, the rest draw
+// each step's xin / sdw rows are staged in LDS and written as whole float4
+// rows (the MFMA layout gives each lane 4 dims of one path, one column off the
+// 16-byte grid): [xin, sdw][path][CP_SROW] (CP_SROW >= Dp).  One step at a
+// time keeps the workgroup's LDS at 93 KB, so a phase-kernel workgroup (63 KB)
+// still fits beside a prefetched rollout on a CU.
+constexpr int CP_SROW = 148;
+constexpr int CP_STAGE = 2 * CP_PATHS * CP_SROW;
 
 typedef float cpf4 __attribute__((ext_vector_type(4)));
 
@@ -207,7 +214,7 @@ __device__ __forceinline__ void corr_draw(const RolloutArgs& p, int m0, int nt4,
 // only draws), K-steps t < 4 O + 4 (the lower triangle; L is zero-padded past
 // nb), everything compile-time so the L fragments stay in registers
 template <int O1, int O2>
-__device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs) {
+__device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs, float* stg) {
   constexpr int NO = (O1 >= 0) + (O2 >= 0);
   constexpr int T1 = O1 >= 0 ? 4 * O1 + 4 : 0, T2 = O2 >= 0 ? 4 * O2 + 4 : 0;
   constexpr int TM = T1 > T2 ? T1 : T2;
@@ -249,6 +256,7 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs) {
   // the K-steps past nb (t >= nt4 up to 4 O + 4) read slots no draw writes:
   // zero both buffers once (0 * stale LDS could be NaN)
   for (int i = threadIdx.x; i < 2 * CP_BUF; i += CP_THREADS) xs[i] = 0.f;
+  for (int i = threadIdx.x; i < CP_STAGE; i += CP_THREADS) stg[i] = 0.f;   // columns never written stay 0
   __syncthreads();
   corr_draw(p, m0, nt4, sqdt, 0, xs);
   __syncthreads();
@@ -294,16 +302,33 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs) {
               fa[oc][r].put(p, m, d, n + 1, t1, dw);
               continue;
             }
-            p.xin[row * p.ldx + 1 + d] = x[oc][r];
+            float* sr = stg + cl * CP_SROW;
+            sr[1 + d] = x[oc][r];
             const float sg = rn_add(rn_mul(p.sig_a, x[oc][r]), p.sig_b);
             const float sv = rn_mul(sg, dw);
-            p.sdw[row * p.ldx + 1 + d] = sv;
+            sr[CP_PATHS * CP_SROW + 1 + d] = sv;
             x[oc][r] = rn_add(rn_add(x[oc][r], rn_mul(rn_mul(p.mu_a, x[oc][r]), dt)), sv);
           }
         if (writes_t && p.out == PATH_ROLLOUT) {
-          p.xin[row * p.ldx] = t0;
-          p.xin[row * p.ldx + p.D + 1] = 1.0f;
+          float* sr = stg + cl * CP_SROW;
+          sr[0] = t0;
+          sr[p.D + 1] = 1.0f;
         }
+        (void)row;
+      }
+      if (p.out == PATH_ROLLOUT) {
+        // this step's rows: every thread of the workgroup, whole float4 columns
+        __syncthreads();
+        const int c4 = p.ldx / 4;
+        for (int it = threadIdx.x; it < 2 * CP_PATHS * c4; it += CP_THREADS) {
+          const int c = it % c4, rest = it / c4, pp = rest % CP_PATHS, arr = rest / CP_PATHS;
+          const int mm = m0 + pp;
+          if (mm >= p.M) continue;
+          const size_t r2 = (size_t)mm * N1 + n;
+          float* dst = arr ? p.sdw : p.xin;
+          *(cpf4*)(dst + r2 * p.ldx + 4 * c) = *(const cpf4*)(stg + (arr * CP_PATHS + pp) * CP_SROW + 4 * c);
+        }
+        __syncthreads();   // the stage is rewritten by the next step
       }
       t0 = t1;
     }
@@ -332,15 +357,16 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs) {
 template <int NBLK>
 __global__ void __launch_bounds__(CP_THREADS) rollout_corr_kernel(RolloutArgs p) {
   __shared__ __attribute__((aligned(16))) float xs[2 * CP_BUF];
+  __shared__ __attribute__((aligned(16))) float stg[CP_STAGE];
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: corr_wave<0, -1>(p, xs); break;
-    case 1: corr_wave<(1 < NBLK ? 1 : -1), -1>(p, xs); break;
-    case 2: corr_wave<(2 < NBLK ? 2 : -1), -1>(p, xs); break;
-    case 3: corr_wave<(3 < NBLK ? 3 : -1), -1>(p, xs); break;
-    case 4: corr_wave<(4 < NBLK ? 4 : -1), -1>(p, xs); break;
-    case 5: corr_wave<(5 < NBLK ? 5 : -1), -1>(p, xs); break;
-    case 6: corr_wave<(6 < NBLK ? 6 : -1), -1>(p, xs); break;
-    default: corr_wave<(7 < NBLK ? 7 : -1), -1>(p, xs); break;
+    case 0: corr_wave<0, -1>(p, xs, stg); break;
+    case 1: corr_wave<(1 < NBLK ? 1 : -1), -1>(p, xs, stg); break;
+    case 2: corr_wave<(2 < NBLK ? 2 : -1), -1>(p, xs, stg); break;
+    case 3: corr_wave<(3 < NBLK ? 3 : -1), -1>(p, xs, stg); break;
+    case 4: corr_wave<(4 < NBLK ? 4 : -1), -1>(p, xs, stg); break;
+    case 5: corr_wave<(5 < NBLK ? 5 : -1), -1>(p, xs, stg); break;
+    case 6: corr_wave<(6 < NBLK ? 6 : -1), -1>(p, xs, stg); break;
+    default: corr_wave<(7 < NBLK ? 7 : -1), -1>(p, xs, stg); break;
   }
 }
 
