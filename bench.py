@@ -11,8 +11,9 @@ All inputs resident in HBM.  value = total SDE path-steps/s over all ranks
     python bench.py [--gpus N] [--steps K] [--warmup W] [--strong]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
---workload basket|hjb|heston runs BASELINE configs 3-5 on this process's GPUs
-(separate lines for DESIGN.md; the headline is the default bsb workload).
+--workload oned|basket|hjb|heston runs BASELINE configs 1 and 3-5 on this
+process's GPUs (separate lines for DESIGN.md; the headline is the default bsb
+workload).
 """
 from __future__ import annotations
 
@@ -75,6 +76,9 @@ WORKLOADS = {
                         "(with_corr_high_dimension_pde.py semantics: Adam, clip 1.0)"),
     "hjb": dict(cls="HamiltonJacobiBellman", D=100, layers=[101] + 4 * [256] + [1], mode="FC", act="Sine",
                 M=2048, N=20, xi="zeros", desc="100-D HJB, FC-Sine [101,256x4,1] (hjb_implement.py semantics)"),
+    "oned": dict(cls="CallOption1D", D=1, layers=[2] + 4 * [256] + [1], mode="FC", act="Sine", M=256, N=50,
+                 xi="ones", desc="1-D Black-Scholes call, FC-Sine [2,256x4,1], batch 256, 50 steps, Q3 squeeze "
+                                 "broadcast active (1d_BSPDE_case.py semantics: Adam, clip 1.0)"),
     "heston": dict(cls="HestonFBSNN", D=50, layers=[51] + 4 * [110] + [1], mode="Naisnet", act="Sine",
                    M=1024, N=100, xi="ones",
                    desc="50-asset Heston (state 100), Naisnet-Sine (heston_dnnpde.py semantics generalised to "
@@ -86,7 +90,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(iters=10, warmup=2):
+def cpu_baseline(iters=30, warmup=2):
     """The oracle's faithful torch-CPU restatement of the reference step
     (fetch_minibatch + loss_function + double backward + Adam, anomaly mode
     off), timed on the host cores: `warmup` untimed iterations, then `iters`
@@ -110,7 +114,9 @@ def cpu_baseline(iters=10, warmup=2):
                       f"N=50, D=100, NAIS-Net 4x110 Sine, Adam) by oracle/fbsnn_ref.py (torch CPU, autograd "
                       f"double backward, dense diag sigma, anomaly off): median {med:.3f} s/iteration, "
                       f"min {min(times):.3f}, max {max(times):.3f}",
-            "s_per_iter": {"median": med, "min": float(min(times)), "max": float(max(times))}}
+            "s_per_iter": {"median": med, "min": float(min(times)), "max": float(max(times)),
+                           "p25": float(np.percentile(times, 25)), "p75": float(np.percentile(times, 75)),
+                           "n": len(times)}}
 
 
 def parity_trajectory(pkg, dev):
@@ -136,7 +142,8 @@ def parity_trajectory(pkg, dev):
         for s, y_ref in zip(tr["steps"], tr["Y0"]):
             m.train(int(s) - done, 1e-3)
             done = int(s)
-            u = float(m.net_u(t0, x0)[0])
+            with torch.no_grad():
+                u = float(m.net_u(t0, x0)[0])
             rows.append({"steps": int(s), "Y0": u, "Y0_reference": float(y_ref), "abs_err": abs(u - float(y_ref))})
     return {"metric": "|u(0,X_0) - reference| after k reference train() steps (same init, same numpy batches)",
             "tolerance": 1e-3, "max_abs_err": max(r["abs_err"] for r in rows), "points": rows}
@@ -186,6 +193,10 @@ def build_model(pkg, wl, M, dev, args):
         return cls(Xi, T, M, wl["N"], Dw, wl["layers"], mode, act, device=dev), Xi
     if wl["cls"] == "HamiltonJacobiBellman":
         return cls(Xi, T, M, wl["N"], Dw, wl["layers"], mode, act, device=dev), Xi
+    if wl["cls"] == "CallOption1D":
+        m = cls(Xi, T, M, wl["N"], Dw, None, wl["layers"], mode, act, device=dev)
+        m.N = wl["N"]
+        return m, Xi
     if wl["cls"] == "BasketCallOption":
         np.random.seed(0)                      # the Q10 correlation matrix draw
         m = cls(Xi, T, M, wl["N"], Dw, None, wl["layers"], mode, act, "random_correlation", device=dev)
@@ -201,7 +212,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--strong", action="store_true", help="global batch fixed at the workload's M (split)")
     ap.add_argument("--workload", default="bsb", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-iters", type=int, default=10)
+    ap.add_argument("--cpu-iters", type=int, default=30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true", help="skip the 100-step Y0 parity trajectory")
     ap.add_argument("--paths-per-gpu", type=int, default=None,
@@ -276,7 +287,8 @@ def main():
     prof = model.solver.profile_read()
     model.solver.profile(False)
 
-    u0, _ = model.net_u(torch.zeros(1), model.Xi.reshape(1, -1))
+    with torch.no_grad():
+        u0, _ = model.net_u(torch.zeros(1), model.Xi.reshape(1, -1))
     u0 = float(u0)
 
     if rank != 0:

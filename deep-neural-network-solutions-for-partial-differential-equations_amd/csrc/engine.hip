@@ -122,6 +122,7 @@ struct dbsde_ctx {
   long long* d_woffs = nullptr;   // NAIS: W_j offsets in the flat params
   float** d_rtr = nullptr;
   float** d_abar = nullptr;
+  float** d_wsnap = nullptr;      // NAIS: W_j as of rtr_params_kernel (read by the projection adjoint)
   double* proj_part = nullptr;
   double* dot_part = nullptr;     // <Abar_j, R_j> partials from the gradient finalize (one per 64 elements)
   int dot_nblk = 0;               // partials slots per block (stride)
@@ -463,11 +464,12 @@ int build_buffers(dbsde_ctx* c) {
   const int LW = c->L[1];
   if (c->proj) {
     if ((rc = dalloc_t(c, &c->norms, (size_t)K + 1))) return rc;
-    std::vector<float*> hr(K), ha(K);
+    std::vector<float*> hr(K), ha(K), hs(K);
     std::vector<long long> hw(K);
     for (int j = 1; j <= K; ++j) {
       if ((rc = dalloc_t(c, &c->rtr[j], (size_t)LW * LW))) return rc;
       if ((rc = dalloc_t(c, &c->abar[j], (size_t)LW * LW))) return rc;
+      if ((rc = dalloc_t(c, &hs[j - 1], (size_t)LW * LW))) return rc;
       hr[j - 1] = c->rtr[j];
       ha[j - 1] = c->abar[j];
       hw[j - 1] = c->B[j - 1].w;
@@ -479,9 +481,11 @@ int build_buffers(dbsde_ctx* c) {
     if ((rc = dalloc_t(c, &c->dot_part, (size_t)K * c->dot_nblk))) return rc;
     if ((rc = dalloc_t(c, &c->d_rtr, K))) return rc;
     if ((rc = dalloc_t(c, &c->d_abar, K))) return rc;
+    if ((rc = dalloc_t(c, &c->d_wsnap, K))) return rc;
     if ((rc = dalloc_t(c, &c->d_woffs, K))) return rc;
     HIPC(c, hipMemcpy(c->d_rtr, hr.data(), K * sizeof(float*), hipMemcpyHostToDevice));
     HIPC(c, hipMemcpy(c->d_abar, ha.data(), K * sizeof(float*), hipMemcpyHostToDevice));
+    HIPC(c, hipMemcpy(c->d_wsnap, hs.data(), K * sizeof(float*), hipMemcpyHostToDevice));
     HIPC(c, hipMemcpy(c->d_woffs, hw.data(), K * sizeof(long long), hipMemcpyHostToDevice));
   }
   if ((rc = dalloc_t(c, &c->d_used, (size_t)c->nparams))) return rc;
@@ -995,7 +999,7 @@ __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs,
 // are staged in LDS with one round of independent loads (a K-tiled loop would
 // chain L/16 dependent global-load latencies).
 __device__ __forceinline__ void rtr_tile(const float* params, const long long* woffs, int L, float* const* rtr,
-                                         double* part, int nblk, int j, int tile) {
+                                         float* const* wsnap, double* part, int nblk, int j, int tile) {
   __shared__ float As[16][NAIS_LMAX + 1];   // As[r][k] = W[k][16 ti + r]
   __shared__ float Bs[NAIS_LMAX][17];       // Bs[k][c] = W[k][16 tj + c]
   const int nt = (L + 15) / 16;
@@ -1012,6 +1016,10 @@ __device__ __forceinline__ void rtr_tile(const float* params, const long long* w
   float v = 0.f;
   for (int k = 0; k < L; ++k) v += As[ty][k] * Bs[k][tx];
   const int row = ti * 16 + ty, col = tj * 16 + tx;
+  // snapshot of W_j before this step's update (one 16 x 16 tile per block):
+  // the fused optimizer update rewrites params while proj_backward_kernel's
+  // other blocks still read W_j
+  if (row < L && col < L) wsnap[j][row * L + col] = W[row * L + col];
   double sq = 0.0;
   if (row < L && col < L) {
     rtr[j][row * L + col] = v;
@@ -1027,8 +1035,8 @@ __device__ __forceinline__ void rtr_tile(const float* params, const long long* w
   if (threadIdx.x == 0) part[j * nblk + tile] = red[0];
 }
 __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, const long long* woffs, int L,
-                                                         float* const* rtr, double* part, int nblk) {
-  rtr_tile(params, woffs, L, rtr, part, nblk, blockIdx.y, blockIdx.x);
+                                                         float* const* rtr, float* const* wsnap, double* part, int nblk) {
+  rtr_tile(params, woffs, L, rtr, wsnap, part, nblk, blockIdx.y, blockIdx.x);
 }
 // NAIS projection adjoint (Functions/naisnet.py:30-39 reversed), one kernel:
 //   Abar_j = dL/dA_j (slab sums), R_j = W_j^T W_j, n = |R_j|_F
@@ -1038,7 +1046,7 @@ __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, co
 // Every block recomputes <Abar_j, R_j> in the same fixed order (L^2 products,
 // cheap), so no separate reduction launch is needed; S = Rbar + Rbar^T is
 // formed on the fly in the B tile of the LDS-tiled GEMM.
-__global__ void __launch_bounds__(256) proj_backward_kernel(const float* params, const long long* woffs,
+__global__ void __launch_bounds__(256) proj_backward_kernel(const float* const* wsnap, const long long* woffs,
                                                             float* const* abar, float* const* rtr, int L,
                                                             const double* proj_part, int proj_n, const double* dot_part,
                                                             int dot_nblk, int dot_nused, float* grad, FusedOpt fo,
@@ -1051,7 +1059,10 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* params,
   const int ti = blockIdx.x / nt, tj = blockIdx.x % nt;
   const float* Ab = abar[j];
   const float* R = rtr[j];
-  const float* W = params + woffs[j];
+  // W_j from the snapshot rtr_params_kernel took: with the fused update, the
+  // blocks (ti, tj') of this launch rewrite params' W_j rows in place while
+  // this block still reads them
+  const float* W = wsnap[j];
   // every operand load in one round, before the scalars are known
   constexpr int PER = NAIS_LMAX * 16 / 256;
   float wv[PER], abs_[PER], rs[PER];
@@ -1115,7 +1126,8 @@ int prep_weights(dbsde_ctx* c, const float* params) {
     const double fl = 2.0 * c->K * LW * (double)LW * LW;
     const int nblk = ((LW + 15) / 16) * ((LW + 15) / 16);
     RUN(c, "rtr", fl, 0.0,
-        rtr_params_kernel<<<dim3(nblk, c->K), 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, c->proj_part, nblk));
+        rtr_params_kernel<<<dim3(nblk, c->K), 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, c->d_wsnap,
+                                                            c->proj_part, nblk));
   }
   RUN(c, "pack_weights", 0.0, 0.0, pack_tagged_kernel<<<dim3(c->prep_blocks, c->n_prep), 256, 0, s>>>(c->d_prep, params, nullptr));
   return DBSDE_OK;
@@ -1210,7 +1222,7 @@ int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double*
     const int LW = c->L[1];
     const int ntile = ((LW + 15) / 16) * ((LW + 15) / 16);
     RUN(c, "proj_backward", 2.0 * c->K * LW * (double)LW * LW, 0.0,
-        proj_backward_kernel<<<dim3(ntile, c->K), 256, 0, s>>>(params, c->d_woffs, c->d_abar, c->d_rtr, LW,
+        proj_backward_kernel<<<dim3(ntile, c->K), 256, 0, s>>>(c->d_wsnap, c->d_woffs, c->d_abar, c->d_rtr, LW,
                                                                c->proj_part, ntile, c->dot_part, c->dot_nblk,
                                                                c->dot_nused, grad, f, fuse));
   }

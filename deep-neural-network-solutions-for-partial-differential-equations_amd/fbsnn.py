@@ -81,8 +81,33 @@ class _NetU(torch.autograd.Function):
         gdu = torch.zeros_like(X) if gdu is None else gdu.float().contiguous()
         g = torch.empty_like(fb.params)
         fb.solver.net_u_vjp(fb.params, t, X, gu, gdu, g)
-        grads = tuple(g[o:o + n].view(shape) for o, n, shape in fb._param_slices())
-        return (None, None, None) + grads
+        return (None, None, None) + fb._param_grads(g)
+
+
+class _Loss(torch.autograd.Function):
+    """FBSNN.loss_function's loss as a graph-connected scalar (the reference
+    returns it with the graph built, DeepBSDE.py:278-279 / nd_BSPDE_case.py:378
+    call loss.backward() on it).  The forward runs dbsde_loss_grad once, which
+    yields the loss and its parameter gradient together; the backward scales
+    that gradient by the incoming cotangent and splits it into the model
+    parameters.  t, W and Xi are not differentiated."""
+
+    @staticmethod
+    def forward(ctx, fb, t, W, Xi, *params):
+        g = torch.empty_like(fb.params)
+        out = fb._run(t, W, Xi, grad=g)
+        ctx.fb = fb
+        ctx.save_for_backward(g)
+        ctx.mark_non_differentiable(out["X"], out["Y"])
+        return out["loss"][0].clone(), out["X"], out["Y"]
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gl, gX, gY):
+        (g,) = ctx.saved_tensors
+        if gl is None:
+            return (None,) * (4 + len(ctx.fb._param_slices()))
+        return (None, None, None, None) + ctx.fb._param_grads(g * gl.float())
 
 
 class FBSNN(ABC):
@@ -257,6 +282,16 @@ class FBSNN(ABC):
         self.solver.net_u(self.params, t, X, u, du)
         return u, du
 
+    def _param_grads(self, g):
+        """A flat gradient split into named_parameters() order; None for a
+        parameter no output depends on (NAIS-Net's input_layers[K]),
+        whose .grad torch autograd leaves None as well."""
+        if getattr(self, "_pused", None) is None:
+            used = self.solver.used_mask
+            self._pused = [bool(used[o:o + n].any()) for o, n, _ in self._param_slices()]
+        return tuple(g[o:o + n].view(shape) if u else None
+                     for (o, n, shape), u in zip(self._param_slices(), self._pused))
+
     def _param_slices(self):
         """(offset, numel, shape) of every model parameter in the flat vector, in
         named_parameters() order (the flat vector is in state_dict order,
@@ -276,7 +311,15 @@ class FBSNN(ABC):
         return torch.autograd.grad(g, X, torch.ones_like(g))[0]
 
     def loss_function(self, t, W, Xi):
-        """nd_BSPDE_case.py:237-281 -> (loss, X, Y, Y[0,0,0])."""
+        """nd_BSPDE_case.py:237-281 -> (loss, X, Y, Y[0,0,0]).  With grad mode
+        on and the model's parameters requiring grad, the loss is connected to
+        them like the reference's: loss.backward() accumulates the native
+        gradient (dbsde_loss_grad) into each parameter's .grad.  X and Y are
+        returned detached."""
+        params = [p for _, p in self.model.named_parameters()]
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            loss, X, Y = _Loss.apply(self, t, W, Xi, *params)
+            return loss, X, Y, Y[0, 0, 0]
         out = self._run(t, W, Xi)
         Y = out["Y"]
         return out["loss"][0], out["X"], Y, Y[0, 0, 0]

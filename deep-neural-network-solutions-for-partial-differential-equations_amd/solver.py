@@ -211,6 +211,10 @@ class NativeSolver:
         does not advance it."""
         if kind not in _lib.OPTIMIZERS:
             raise ValueError(f"Optimizer type '{kind}' is not recognized.")
+        if kind == "ASGD" and step_state is None and not asgd_eta:
+            # without the device step counter ASGD's eta / mu come from the
+            # caller; eta = 0 would silently leave the parameters unchanged
+            raise ValueError("ASGD needs step_state (device step counter) or an explicit asgd_eta > 0")
         for name, v_ in (("params", params), ("grad", grad), ("m", m), ("v", v)):
             self._check_tensor(v_, name, self.nparams)
         self._check_tensor(skip_nonfinite_loss, "loss", 1)

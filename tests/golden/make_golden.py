@@ -444,8 +444,31 @@ def round3_cases(mods):
           flush=True)
 
 
+def round4_cases(mods):
+    """Round 4: BASELINE config 1 -- the 1-D call of 1d_BSPDE_case.py
+    (CallOption, 1d_BSPDE_case.py:510-560) with FC-Sine [2,256x4,1], the
+    network of its __main__ (:993-1006), at M > 1 so that the D == 1 squeeze
+    broadcast (Q3, :271-273) is active: a small case (M = 16, N = 5) and the
+    config's full shape (M = 256, N = 50)."""
+    import torch
+    layers = [2] + 4 * [256] + [1]
+    for k, (M, N, full_z) in enumerate([(16, 5, True), (256, 50, False)]):
+        seed = 600 + k
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        with contextlib.redirect_stdout(io.StringIO()):
+            obj = mods["oned"].CallOption(np.array([[1.0]]), 1.0, M, N, 1, 5.0, layers, "FC", "Sine")
+        params = _flat(obj.model.state_dict())
+        res = _run_case(obj, M, N, 1, full_z=full_z)
+        _save_case(f"w256_oned_call_FC_Sine_M{M}_N{N}", "call1d", "FC", "Sine", layers, np.array([[1.0]]), M, N,
+                   seed, params, res)
+
+
 if __name__ == "__main__":
     m = _setup()
+    if "--round4-only" in sys.argv:
+        round4_cases(m)
+        sys.exit(0)
     if "--round3-only" in sys.argv:
         round3_cases(m)
         sys.exit(0)
@@ -457,6 +480,7 @@ if __name__ == "__main__":
         heston_cases(m)
         sys.exit(0)
     small_cases(m)
+    round4_cases(m)
     train_cases(m)
     wide_cases(m)
     heston_cases(m)

@@ -119,7 +119,8 @@ def test_loss_grad_matches_reference(pkg, dev, path, fused):
         np.testing.assert_array_equal(r["X"], g["X"])
     np.testing.assert_allclose(r["loss"][0], g["loss"], rtol=1e-4)
     np.testing.assert_allclose(r["Y"], g["Y"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Y"]).max()))
-    np.testing.assert_allclose(r["Z"], g["Z"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Z"]).max()))
+    if "Z" in g:                                   # full-shape fixtures store no Z
+        np.testing.assert_allclose(r["Z"], g["Z"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Z"]).max()))
     used = g["used"]
     assert np.all(r["grad"][~used] == 0)
     np.testing.assert_allclose(r["grad"][used], g["grad"][used], rtol=0, atol=2e-4 * np.abs(g["grad"]).max())

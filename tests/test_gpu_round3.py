@@ -246,7 +246,7 @@ def test_lbfgs_train_matches_reference(pkg, dev):
     graph, min_loss, _ = m.train(int(g["iters"]), float(g["lr"]), optimizer_type="LBFGS")
     np.testing.assert_allclose(min_loss, float(g["min_loss"]), rtol=1e-4)
     p1 = g["params1"]
-    np.testing.assert_allclose(m.params.cpu().numpy(), p1, rtol=0, atol=2e-3 * np.abs(p1).max())
+    np.testing.assert_allclose(m.params.cpu().numpy(), p1, rtol=0, atol=2e-4 * np.abs(p1).max())
 
 
 # --------------------------------------------------------------------------- optimizer / batches

@@ -46,7 +46,8 @@ def test_restatement_matches_reference(path):
     np.testing.assert_array_equal(res["X"], g["X"])          # the rollout is bit-exact
     np.testing.assert_allclose(res["loss"], g["loss"], rtol=1e-6)
     np.testing.assert_allclose(res["Y"], g["Y"], rtol=1e-6, atol=1e-6)
-    np.testing.assert_allclose(res["Z"], g["Z"], rtol=1e-5, atol=1e-6)
+    if "Z" in g:                                              # full-shape fixtures store no Z
+        np.testing.assert_allclose(res["Z"], g["Z"], rtol=1e-5, atol=1e-6)
     np.testing.assert_array_equal(res["used"], g["used"])
     scale = np.abs(g["grad"]).max()
     np.testing.assert_allclose(res["grad"], g["grad"], rtol=0, atol=1e-5 * scale)
@@ -66,7 +67,8 @@ def test_timeparallel_matches_reference(path):
     np.testing.assert_allclose(out["loss"], g["loss"], rtol=2e-5)
     np.testing.assert_allclose(out["X"], g["X"], rtol=1e-6, atol=1e-6 * max(1.0, np.abs(g["X"]).max()))
     np.testing.assert_allclose(out["Y"], g["Y"], rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(out["Z"], g["Z"], rtol=1e-4, atol=1e-5)
+    if "Z" in g:
+        np.testing.assert_allclose(out["Z"], g["Z"], rtol=1e-4, atol=1e-5)
     used = g["used"]
     scale = np.abs(g["grad"]).max()
     np.testing.assert_allclose(out["grad"][used], g["grad"][used], rtol=0, atol=1e-4 * scale)
