@@ -25,6 +25,7 @@
 #include "kernels.hpp"
 #include "paths.hpp"
 #include "phase.hpp"
+#include "phase2.hpp"
 #include "chainx3.hpp"
 #include "tnx3.hpp"
 #include "tnw.hpp"
@@ -157,6 +158,7 @@ struct dbsde_ctx {
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
   bool x3 = false;                // ... in their split-bf16 form (phase.hpp)
+  bool nt2 = false;               // ... with two 16-row tiles per wave where built (phase2.hpp; DBSDE_NT=2)
   bool x3chain = false;           // per-layer chain GEMMs in split-bf16 form (chainx3.hpp)
   // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
   // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
@@ -278,27 +280,35 @@ int join_side(dbsde_ctx* c, int i) {
 // fused phase-kernel instantiations: (level tiles T, D tiles TD, blocks K)
 struct FusedVariant {
   int T, TD, K, act, hv, x3;
+  int rows;   // rows per workgroup: 64 (phase.hpp, one 16-row tile per wave) or 128 (phase2.hpp, two)
   void (*A)(FusedArgs);
   void (*C)(FusedArgs);
 };
 // HV: the network has the NAIS x-stack (V_j); a template flag, so each kernel
 // carries only its own code path (smaller straight-line kernels).  X3: the
 // split-bf16 matrix-core form (phase.hpp), at width 110/112; the fp32-input
-// MFMA form stays selectable (DBSDE_X3=0) and serves width 16.
+// MFMA form stays selectable (DBSDE_X3=0) and serves width 16.  The two-tile
+// kernels (phase2.hpp) exist for the split-bf16 width-112 networks.
 #define FV(T, TD, K, ACT, HV, X3) \
-  {T, TD, K, ACT, HV, X3, phaseA_kernel<T, TD, K, ACT, HV, X3>, phaseC_kernel<T, TD, K, ACT, HV, X3>}
+  {T, TD, K, ACT, HV, X3, P3_ROWS, phaseA_kernel<T, TD, K, ACT, HV, X3>, phaseC_kernel<T, TD, K, ACT, HV, X3>}
 #define FV2(T, TD, K, ACT, X3) FV(T, TD, K, ACT, true, X3), FV(T, TD, K, ACT, false, X3)
+#define FQ(T, K, ACT, HV) {T, T, K, ACT, HV, 1, Q_ROWS, phaseA2_kernel<T, K, ACT, HV>, phaseC2_kernel<T, K, ACT, HV>}
+#define FQ2(T, K, ACT) FQ(T, K, ACT, true), FQ(T, K, ACT, false)
 const FusedVariant kFused[] = {
+    FQ2(7, 3, 0), FQ2(7, 3, 1), FQ2(7, 3, 2),
     FV2(7, 7, 3, 0, 1), FV2(7, 7, 3, 1, 1), FV2(7, 7, 3, 2, 1), FV2(7, 7, 3, 0, 0), FV2(7, 7, 3, 1, 0),
     FV2(7, 7, 3, 2, 0), FV2(1, 1, 1, 0, 0), FV2(1, 1, 1, 1, 0), FV2(1, 1, 1, 2, 0), FV2(1, 1, 2, 0, 0),
     FV2(1, 1, 2, 1, 0), FV2(1, 1, 2, 2, 0), FV2(1, 1, 3, 0, 0), FV2(1, 1, 3, 1, 0), FV2(1, 1, 3, 2, 0),
 };
+#undef FQ2
+#undef FQ
 #undef FV2
 #undef FV
-int fused_variant(int T, int TD, int K, int act, bool hv, bool x3) {
+// rows_max: 128 admits the two-tile kernels (preferred), 64 only the one-tile ones
+int fused_variant(int T, int TD, int K, int act, bool hv, bool x3, int rows_max = P3_ROWS) {
   for (int i = 0; i < (int)(sizeof(kFused) / sizeof(kFused[0])); ++i)
     if (kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv &&
-        kFused[i].x3 == (int)x3)
+        kFused[i].x3 == (int)x3 && kFused[i].rows <= rows_max)
       return i;
   return -1;
 }
@@ -400,6 +410,8 @@ int build_net(dbsde_ctx* c) {
   const bool allow = !(env && env[0] == '0');
   const char* ex3 = getenv("DBSDE_X3");
   const bool want_x3 = !(ex3 && ex3[0] == '0');
+  const char* ent = getenv("DBSDE_NT");
+  c->nt2 = ent && ent[0] == '2';
   c->x3 = want_x3 && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, true) >= 0;
   c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3) >= 0;
   c->x3 = c->x3 && c->fused;
@@ -805,7 +817,7 @@ void x3_weights(dbsde_ctx* c, ChainArgs& a, const float* img, int tout, int ti) 
   a.x3_ti = ti;
 }
 
-constexpr int ROW_PAD = P3_ROWS;   // rows per phase-kernel workgroup (a multiple of the chain-GEMM tile, 64)
+constexpr int ROW_PAD = Q_ROWS;    // rows per phase-kernel workgroup (a multiple of the chain-GEMM tile, 64)
 
 RolloutArgs rollout_args(dbsde_ctx* c, const dbsde_batch* b) {
   const dbsde_problem& pr = c->cfg.problem;
@@ -1804,7 +1816,8 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   int nloss_parts;
   bool tnw_piped = false;
   FusedArgs fa;
-  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act, c->has_v, c->x3) : -1;
+  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act, c->has_v, c->x3,
+                                          c->nt2 ? Q_ROWS : P3_ROWS) : -1;
   if (fv >= 0) {
     fa = fused_args(c, R, Rp, N1, q3);
     if (!fused_piece_counts_ok(c, fa)) return fail(c, DBSDE_EINVAL, "internal: fused kernel piece counts");
@@ -1813,18 +1826,19 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     const double byA = 4.0 * R * (c->Dp + 4.0 * S + 8.0);
     const double flC = 2.0 * R * ((double)nv * D + 2.0 * K * L[1] * (double)L[1]);
     const double byC = 4.0 * R * (4.0 * c->Dp + 5.0 * S);
-    // chunks of whole paths and whole P3_ROWS-row tiles (P3_ROWS paths =
-    // P3_ROWS (N+1) rows = N+1 tiles)
+    // chunks of whole paths and whole WR-row tiles (WR paths = WR (N+1) rows =
+    // N+1 tiles), WR = the variant's rows per workgroup
+    const int WR = kFused[fv].rows;
     int nch = grad ? c->chunks : 1;
-    while (nch > 1 && (M % P3_ROWS != 0 || (M / P3_ROWS) % nch != 0)) --nch;
+    while (nch > 1 && (M % WR != 0 || (M / WR) % nch != 0)) --nch;
     if (nch <= 1) {
-      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+      RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));
     } else {
       // phase A / phase C of chunk i on stream (i even ? main : pipe2); the
       // two phases are timed as one pipelined segment
-      // chunk sizes in units of P3_ROWS paths; DBSDE_CHUNK0 sets the first chunk's
+      // chunk sizes in units of WR paths; DBSDE_CHUNK0 sets the first chunk's
       // units (the rest split evenly), else all chunks are equal
-      const int units = M / P3_ROWS, utile = N1;   // P3_ROWS paths = N1 tiles
+      const int units = M / WR, utile = N1;   // WR paths = N1 tiles
       std::vector<int> cu(nch, units / nch);
       if (c->chunk0 > 0 && c->chunk0 < units && nch == 2) {
         cu[0] = c->chunk0;
@@ -1842,7 +1856,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       int sb = 0;   // first slice of chunk 1
       {
         const int S = c->tnw_S, n32 = Rp / 32;
-        const long long crow = (long long)cu[0] * utile * P3_ROWS;
+        const long long crow = (long long)cu[0] * utile * WR;
         for (int k = 8; k < S && !sb; k += 8)
           if (32LL * ((long long)k * n32 / S) == crow) sb = k;
         tnw_piped = grad && c->tnw && !c->prof && nch == 2 && np == 2 && Rp % 32 == 0 && sb > 0;
@@ -1881,8 +1895,8 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     }
     if (grad) {
       if (nch <= 1)
-        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
-      nloss_parts = Rp / P3_ROWS;
+        RUN(c, "fused_tangent_reverse", flC, byC, kFused[fv].C<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));
+      nloss_parts = Rp / WR;
     } else {
       RUN(c, "loss_rows", 0.0, 4.0 * R * 3.0 * D,
           cotan_kernel<<<Rp / 16, 256, 0, s>>>(cotan_params(c, R, Rp, N1, q3), c->loss_part));
@@ -2077,7 +2091,8 @@ int dbsde_net_u_vjp(dbsde_ctx* c, const float* params, int R, const float* t, co
   const unsigned nb = (unsigned)((n + 255) / 256);
   RUN(c, "netu_input", 0.0, 0.0, netu_input_kernel<<<nb, 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
   if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
-  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3) : -1;
+  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3,
+                                          c->nt2 ? Q_ROWS : P3_ROWS) : -1;
   if (fv >= 0) {
     // ubar -> rres rows, zbar -> the sdw rows phase C reads (phase A's use of
     // sdw only feeds the residual row sums, unused here)
@@ -2087,8 +2102,9 @@ int dbsde_net_u_vjp(dbsde_ctx* c, const float* params, int R, const float* t, co
     if (!fused_piece_counts_ok(c, fa)) return fail(c, DBSDE_EINVAL, "internal: fused kernel piece counts");
     fa.cp.ext = 1;
     fa.cp.ext_ub = c->rres;
-    RUN(c, "fused_fwd_inputgrad", 0.0, 0.0, kFused[fv].A<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
-    RUN(c, "fused_tangent_reverse", 0.0, 0.0, kFused[fv].C<<<Rp / P3_ROWS, 64 * P3_WAVES, 0, s>>>(fa));
+    const int WR = kFused[fv].rows;
+    RUN(c, "fused_fwd_inputgrad", 0.0, 0.0, kFused[fv].A<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));
+    RUN(c, "fused_tangent_reverse", 0.0, 0.0, kFused[fv].C<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));
   } else {
     if ((rc = forward_and_inputgrad(c, R, Rp, false))) return rc;
     RUN(c, "vjp_cotangents", 0.0, 0.0,

@@ -194,6 +194,7 @@ __device__ __forceinline__ float col_zbar(const CotanParams& p, const RowCotan& 
 
 // Forward-only loss (predict / loss_function without backward): per-block
 // partial sums of the row losses; 16 threads per row, 16 rows per block.
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) cotan_kernel(CotanParams p, double* loss_part) {
   const int sub = threadIdx.x & 15;
   const int r = blockIdx.x * 16 + (threadIdx.x >> 4);
@@ -219,5 +220,6 @@ __global__ void __launch_bounds__(256) cotan_kernel(CotanParams p, double* loss_
   }
   if (threadIdx.x == 0) loss_part[blockIdx.x] = red[0];
 }
+#endif
 
 }  // namespace dbsde

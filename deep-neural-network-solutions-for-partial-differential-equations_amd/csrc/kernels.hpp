@@ -397,6 +397,7 @@ __global__ void __launch_bounds__(256) chain_gemm_kernel(ChainArgs p) {
 // --------------------------------------------------------------------------
 // u = h . w_out + b_out   (one 16-lane group per row)
 // --------------------------------------------------------------------------
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) rowdot_kernel(const float* H, int ldh, int ncols, const float* w,
                                                      const float* b, float* u, int Rp, float* umask) {
   const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
@@ -415,9 +416,11 @@ __global__ void __launch_bounds__(256) rowdot_kernel(const float* H, int ldh, in
     }
   }
 }
+#endif
 
 // ubar[row] from the per-row residuals; loss partial sums per block.
 // rres[r] = Y_{n+1} - Ytilde_{n+1} (n < N), or Y_N - g(X_N) (n == N).
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) ubar_kernel(const float* rres, const float* xin, int ldx, int R, int Rp,
                                                    int N1, float phi_r, const float* lossrow, float* ubar,
                                                    float* u16, double* loss_part, const float* umask) {
@@ -449,11 +452,13 @@ __global__ void __launch_bounds__(256) ubar_kernel(const float* rres, const floa
   }
   if (threadIdx.x == 0) loss_part[blockIdx.x] = red[0];
 }
+#endif
 
 // net_u VJP inputs (dbsde_net_u_vjp): the caller's ubar [R] and zbar [R, D]
 // as row buffers -- ub [Rp] (zero past R) and z rows [Rp, ldz] (columns
 // 1..D, zero elsewhere).  With umask (the per-layer form, Heston u-clamp) the
 // values are masked here and u16 (the output-layer operand) is written too.
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) ext_cotan_kernel(const float* ubar, const float* zbar, int R, int Rp, int D,
                                                         int ldz, const float* umask, float* ub, float* zrows,
                                                         float* u16) {
@@ -470,7 +475,9 @@ __global__ void __launch_bounds__(256) ext_cotan_kernel(const float* ubar, const
     if (u16) u16[(size_t)i * 16] = v;
   }
 }
+#endif
 
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) loss_final_kernel(const double* part, int n, float* loss) {
   __shared__ double red[256];
   double a = 0.0;
@@ -483,6 +490,7 @@ __global__ void __launch_bounds__(256) loss_final_kernel(const double* part, int
   }
   if (threadIdx.x == 0) loss[0] = (float)red[0];
 }
+#endif
 
 // --------------------------------------------------------------------------
 // TN reduction GEMM for parameter gradients:
@@ -509,6 +517,7 @@ struct TNArgs {
 constexpr int TN_KC = 16;
 constexpr int TN_LS = 80;
 
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) tn_gemm_kernel(TNArgs args) {
   const TNProb& P = args.prob[blockIdx.z];
   const int tile = blockIdx.x;
@@ -594,11 +603,14 @@ __global__ void __launch_bounds__(256) tn_gemm_kernel(TNArgs args) {
         C[(size_t)m * ldc + n] = acc[x][y][j];
       }
 }
+#endif
 
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) fill_col0_kernel(float* buf, int ld, long long rows, float v) {
   const long long r = blockIdx.x * 256LL + threadIdx.x;
   if (r < rows) buf[r * ld] = v;
 }
+#endif
 
 // --------------------------------------------------------------------------
 // Descriptor-driven gather/scatter (weight packing, gradient finalize)
@@ -661,6 +673,7 @@ __host__ __device__ __forceinline__ long long frag_off(int o, int i, int tin, in
 // --------------------------------------------------------------------------
 // clip_grad_norm_ + Adam/AdamW/SGD (nd_BSPDE_case.py:383-384; torch defaults)
 // --------------------------------------------------------------------------
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) sqnorm_kernel(const float* g, const unsigned char* used, long long n,
                                                      double* part) {
   __shared__ double red[256];
@@ -675,6 +688,7 @@ __global__ void __launch_bounds__(256) sqnorm_kernel(const float* g, const unsig
   }
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
+#endif
 
 // optimizer kinds (include/dbsde.h DBSDE_OPT_*), each in torch.optim's
 // single-tensor formula order (the reference's CPU path; torch 2.10)
@@ -785,6 +799,7 @@ __device__ __forceinline__ void opt_update(const OptArgs& a, long long i, float 
   }
 }
 
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float* m, float* v, const unsigned char* used,
                                                     long long n, const double* part, OptArgs a) {
   __shared__ float clip_s;
@@ -821,6 +836,7 @@ __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float*
     opt_update(a, i, gi, prm, m, v);
   }
 }
+#endif
 
 // The optimizer folded into the gradient finalize (single process, no clip,
 // no NaN skip, device step counter): every finalize thread that writes the
@@ -846,6 +862,7 @@ __device__ __forceinline__ void fused_opt_prologue(FusedOpt& fo, bool step_write
 // --------------------------------------------------------------------------
 // output export: rows -> reference layouts
 // --------------------------------------------------------------------------
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) export_kernel(const float* xin, const float* zfull, int ldx, const float* u,
                                                      int R, int D, float* X, float* Y, float* Z) {
   const long long i = blockIdx.x * 256LL + threadIdx.x;
@@ -856,8 +873,10 @@ __global__ void __launch_bounds__(256) export_kernel(const float* xin, const flo
   if (Z) Z[i] = zfull[r * ldx + 1 + d];
   if (Y && d == 0) Y[r] = u[r];
 }
+#endif
 
 // net_u input rows: xin[r] = [t_r, X_r, 1, 0..]
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) netu_input_kernel(const float* t, const float* X, int R, int D, int ldx,
                                                          float* xin) {
   const long long i = blockIdx.x * 256LL + threadIdx.x;
@@ -870,10 +889,12 @@ __global__ void __launch_bounds__(256) netu_input_kernel(const float* t, const f
   else if (c == D + 1) v = 1.f;
   xin[i] = v;
 }
+#endif
 
 // grad[...] = scale * sum_k slab_k[...] for each PK_SLABSUM descriptor:
 // 64 elements per block, the slabs split over 4 thread groups whose fp64
 // partials are added in a fixed order.
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, float* grad) {
   const PackDesc& d = descs[blockIdx.y];
   const int total = d.rows * d.cols;
@@ -923,6 +944,7 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
     }
   }
 }
+#endif
 
 // Weight-gradient finalize of the wave-owned tiles (tnw.hpp): one pass over
 // each problem's T x T slab tile, float4 per lane (whole 128-byte lines, no
@@ -931,6 +953,7 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
 // descriptor window that covers it (W, biases, Abar + its <Abar, R> partial).
 // grid (ceil(T*T / 256), P + 1): y = P zero-fills the nslab == 0 windows.
 constexpr int TF_ELEMS = 256;   // elements per block (64 lanes x float4)
+#ifndef DBSDE_DEVICE_HELPERS_ONLY
 __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int ndesc, const float* slab, int S,
                                                       int P, int T, float* grad, const double* loss_part, int nloss,
                                                       float* loss, FusedOpt fo, int fuse) {
@@ -1037,5 +1060,6 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
     if (lane == 0) dotd->dot_part[blockIdx.x] = dp;
   }
 }
+#endif
 
 }  // namespace dbsde

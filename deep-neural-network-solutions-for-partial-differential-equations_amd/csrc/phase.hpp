@@ -610,8 +610,11 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
   // register limit without it)
   constexpr bool PFC_T = !X3 || (HV && ACT != ACT_TANH), PFC_R = false;   // tanh: register-bound
   constexpr int TB = T > TD ? T : TD, BUF = X3 ? 3 * TB * 64 : ((TB + 1) / 2) * TB * 64;
-  __shared__ floatx4 wl[(X3 ? P3_NBUF_X3 : 2) * BUF];
-  __shared__ double lsum[P3_WAVES];
+  // ONE __shared__ array: with a second LDS object beside the LDS-DMA ring
+  // hipcc waits vmcnt(0) before the first ds_read of every piece (the wave's
+  // prefetched DMAs drained; cdna_hip_programming.md 5, trap 4(a))
+  __shared__ floatx4 wl[(X3 ? P3_NBUF_X3 : 2) * BUF + P3_WAVES / 2];
+  double* lsum = (double*)(wl + (X3 ? P3_NBUF_X3 : 2) * BUF);
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = blockIdx.x + p.tile0;   // 64-row tile (chunked launches offset it)

@@ -54,14 +54,23 @@ __device__ __forceinline__ floatx4 mfma_bf(const bf16x8& a, const bf16x8& b, flo
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Operand loads through buffer descriptors: per lane one 32-bit byte offset
+// (row, column i), the eight rows j of a lane's k group as SGPR offsets
+// j * ld and the 16-column block m as the instruction's immediate offset, so
+// a load costs no address arithmetic (the flat form spent a 64-bit add per
+// load: 234 v_lshl_add_u64 per 294 MFMAs).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
 template <int NB>
-__device__ __forceinline__ void load_cols(float (&r)[NB][8], const float* X, int ld, int row0, int i) {
+__device__ __forceinline__ void load_cols(float (&r)[NB][8], __amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned ld4) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float* p = X + (size_t)(row0 + j) * ld + i;
+  for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int m = 0; m < NB; ++m) r[m][j] = p[16 * m];
-  }
+    for (int m = 0; m < NB; ++m) r[m][j] = bload1(rs, voff + 64u * m, (unsigned)j * ld4);
 }
 
 // acc += A1[rows]^T B1[rows] + A2[rows]^T B2[rows] over 32-row steps
@@ -76,24 +85,26 @@ __device__ __forceinline__ void load_cols(float (&r)[NB][8], const float* X, int
 template <int NB>
 __device__ __forceinline__ void x3_products(floatx4 (&acc)[NB][NB], const TNWProb& pr, int g0, int g1, int i, int q) {
   const int n = g1 - g0, last = 2 * n - 1;
+  const __amdgpu_buffer_rsrc_t rA1 = rsrc_of(pr.A1), rA2 = rsrc_of(pr.A2), rB1 = rsrc_of(pr.B1), rB2 = rsrc_of(pr.B2);
+  const unsigned lda1 = 4u * pr.lda1, lda2 = 4u * pr.lda2, ldb1 = 4u * pr.ldb1, ldb2 = 4u * pr.ldb2;
   float ra[NB][8], rb[NB][8];
-  load_cols<NB>(rb, pr.B1, pr.ldb1, 32 * g0 + 8 * q, i);
-  load_cols<NB>(ra, pr.A1, pr.lda1, 32 * g0 + 8 * q, i);
+  load_cols<NB>(rb, rB1, ((32 * g0 + 8 * q) * ldb1) + 4u * i, ldb1);
+  load_cols<NB>(ra, rA1, ((32 * g0 + 8 * q) * lda1) + 4u * i, lda1);
   Split3 sa = split8(ra[0]);   // A block 0 of the step (the last region splits the next step's)
   for (int k = 0; k <= last; ++k) {
     // the next step (clamped prefetch, unused past the end): product and row
     const int kn = min(k + 1, last), second = kn >= n;
-    const float* A = second ? pr.A2 : pr.A1;
-    const float* B = second ? pr.B2 : pr.B1;
-    const int lda = second ? pr.lda2 : pr.lda1, ldb = second ? pr.ldb2 : pr.ldb1;
-    const int nrow = 32 * (g0 + (second ? kn - n : kn)) + 8 * q;
+    const __amdgpu_buffer_rsrc_t rA = second ? rA2 : rA1, rB = second ? rB2 : rB1;
+    const unsigned lda = second ? lda2 : lda1, ldb = second ? ldb2 : ldb1;
+    const unsigned nrow = 32 * (g0 + (second ? kn - n : kn)) + 8 * q;
+    const unsigned voa = nrow * lda + 4u * i, vob = nrow * ldb + 4u * i;
     Split3 sb[NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) sb[n] = split8(rb[n]);
     __builtin_amdgcn_sched_barrier(0);
-    load_cols<NB>(rb, B, ldb, nrow, i);
+    load_cols<NB>(rb, rB, vob, ldb);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) ra[0][j] = A[(size_t)(nrow + j) * lda + i];
+    for (int j = 0; j < 8; ++j) ra[0][j] = bload1(rA, voa, (unsigned)j * lda);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int m = 0; m < NB; ++m) {
@@ -102,7 +113,7 @@ __device__ __forceinline__ void x3_products(floatx4 (&acc)[NB][NB], const TNWPro
       const Split3 san = split8(ra[m + 1 < NB ? m + 1 : 0]);
       if (m + 1 < NB) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ra[m + 1][j] = A[(size_t)(nrow + j) * lda + 16 * (m + 1) + i];
+        for (int j = 0; j < 8; ++j) ra[m + 1][j] = bload1(rA, voa + 64u * (m + 1), (unsigned)j * lda);
       }
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
@@ -133,7 +144,8 @@ __global__ void __launch_bounds__(256, 1) tnw_x3_kernel(TNWArgs a) {
   const int wg = blockIdx.x, wpg = a.P / 4;
   const int xcd = wg & 7, local = wg >> 3;
   const int s = a.s0 + (local / wpg) * 8 + xcd;
-  const int p = (local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6);
+  // wave-uniform problem index (its operand pointers go to SGPR buffer descriptors)
+  const int p = __builtin_amdgcn_readfirstlane((local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6));
   const TNWProb& pr = a.prob[p];
   const int lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
   const int n32 = a.nchunk / 2;

@@ -57,15 +57,17 @@ def dev():
     return torch.device("cuda:0")
 
 
-def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True):
+def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=2):
     """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at
     create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0); x3=False
     the fp32-input MFMA form of the fused phase and weight-gradient kernels
-    (DBSDE_X3=0 / DBSDE_TNW_X3=0) instead of the split-bf16 one."""
+    (DBSDE_X3=0 / DBSDE_TNW_X3=0) instead of the split-bf16 one; nt=1 the
+    one-tile-per-wave phase kernels (DBSDE_NT=1) where the two-tile ones
+    (phase2.hip) exist."""
     layers = [int(v) for v in g["layers"]]
     D = layers[0] - 1
     env = {"DBSDE_FUSED": "1" if fused else "0", "DBSDE_TNW": "1" if tnw else "0",
-           "DBSDE_X3": "1" if x3 else "0", "DBSDE_TNW_X3": "1" if x3 else "0"}
+           "DBSDE_X3": "1" if x3 else "0", "DBSDE_TNW_X3": "1" if x3 else "0", "DBSDE_NT": str(nt)}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -79,10 +81,10 @@ def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True):
                 os.environ[k] = v
 
 
-def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True):
+def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, nt=2):
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
-    s = make_solver(pkg, dev, g, fused, x3=x3)
+    s = make_solver(pkg, dev, g, fused, x3=x3, nt=nt)
     params = torch.from_numpy(g["params"]).to(dev)
     out = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (N + 1) * D, device=dev),
                Y=torch.empty(M * (N + 1), device=dev), Z=torch.empty(M * (N + 1) * D, device=dev))
@@ -101,14 +103,16 @@ def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True):
     return res
 
 
-@pytest.mark.parametrize("fused", ["fused", "fused_fp32", "chain"])
+@pytest.mark.parametrize("fused", ["fused", "fused_nt1", "fused_fp32", "chain"])
 @pytest.mark.parametrize("path", G1, ids=[os.path.basename(p)[3:-4] for p in G1])
 def test_loss_grad_matches_reference(pkg, dev, path, fused):
     """fused: the default fused kernels (split-bf16 matrix form at width
-    110/112); fused_fp32: the same kernels on fp32-input MFMA; chain: the
+    110/112, two 16-row tiles per wave); fused_nt1: the same with one tile
+    per wave; fused_fp32: the fused kernels on fp32-input MFMA; chain: the
     per-layer GEMM path."""
     g = _load(path)
-    r = native_case(pkg, dev, g, fused=fused != "chain", x3=fused == "fused")
+    r = native_case(pkg, dev, g, fused=fused != "chain", x3=fused in ("fused", "fused_nt1"),
+                    nt=1 if fused == "fused_nt1" else 2)
     if str(g["problem"]) == "heston":
         # the reference's torch.sqrt on the CPU is MKL vsSqrt (ATen vml), which
         # is not correctly rounded at near-ties; the kernel's sqrt is (as numpy's,
