@@ -159,6 +159,8 @@ struct dbsde_ctx {
   bool fused = false;             // wave-level fused phase kernels usable for this net
   bool x3 = false;                // ... in their split-bf16 form (phase.hpp)
   bool nt2 = false;               // ... with two 16-row tiles per wave where built (phase2.hpp; DBSDE_NT=2)
+  bool adot = false;              // ... phase C with adot in memory where both forms exist (DBSDE_ADOT=1)
+  int fv = -1;                    // the fused variant (kFused index) or -1
   bool x3chain = false;           // per-layer chain GEMMs in split-bf16 form (chainx3.hpp)
   // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
   // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
@@ -280,37 +282,50 @@ int join_side(dbsde_ctx* c, int i) {
 // fused phase-kernel instantiations: (level tiles T, D tiles TD, blocks K)
 struct FusedVariant {
   int T, TD, K, act, hv, x3;
-  int rows;   // rows per workgroup: 64 (phase.hpp, one 16-row tile per wave) or 128 (phase2.hpp, two)
+  int rows;     // rows per workgroup: 64 (phase.hpp, or phase2 with one tile per wave) or 128 (phase2, two)
+  int adot;     // phase C keeps adot_j in memory (phase2 ADOT)
+  int xfirst;   // phase C image order: every x-stack image first (X0, X1..XK, F1..FK, B_K..B1)
   void (*A)(FusedArgs);
   void (*C)(FusedArgs);
 };
 // HV: the network has the NAIS x-stack (V_j); a template flag, so each kernel
 // carries only its own code path (smaller straight-line kernels).  X3: the
 // split-bf16 matrix-core form (phase.hpp), at width 110/112; the fp32-input
-// MFMA form stays selectable (DBSDE_X3=0) and serves width 16.  The two-tile
-// kernels (phase2.hpp) exist for the split-bf16 width-112 networks.
-#define FV(T, TD, K, ACT, HV, X3) \
-  {T, TD, K, ACT, HV, X3, P3_ROWS, phaseA_kernel<T, TD, K, ACT, HV, X3>, phaseC_kernel<T, TD, K, ACT, HV, X3>}
+// MFMA form stays selectable (DBSDE_X3=0) and serves width 16.  phase2.hpp:
+// the width-112 networks with two tiles per wave (DBSDE_NT=2; DBSDE_ADOT=1 the
+// adot-in-memory phase C) and config 4's FC width 256.
+#define FV(T, TD, K, ACT, HV, X3)                                                                      \
+  {T, TD, K, ACT, HV, X3, P3_ROWS, 0, (X3) && (HV), phaseA_kernel<T, TD, K, ACT, HV, X3>, \
+   phaseC_kernel<T, TD, K, ACT, HV, X3>}
 #define FV2(T, TD, K, ACT, X3) FV(T, TD, K, ACT, true, X3), FV(T, TD, K, ACT, false, X3)
-#define FQ(T, K, ACT, HV) {T, T, K, ACT, HV, 1, Q_ROWS, phaseA2_kernel<T, K, ACT, HV>, phaseC2_kernel<T, K, ACT, HV>}
-#define FQ2(T, K, ACT) FQ(T, K, ACT, true), FQ(T, K, ACT, false)
+#define FQ(T, TD, K, ACT, HV, NT, NBUF, ADOT)                                                              \
+  {T, TD, K, ACT, HV, 1, 64 * NT, ADOT, (HV) && !(ADOT), phaseA2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>, \
+   phaseC2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>},
 const FusedVariant kFused[] = {
-    FQ2(7, 3, 0), FQ2(7, 3, 1), FQ2(7, 3, 2),
+    DBSDE_PHASE2_INSTANCES(FQ)
     FV2(7, 7, 3, 0, 1), FV2(7, 7, 3, 1, 1), FV2(7, 7, 3, 2, 1), FV2(7, 7, 3, 0, 0), FV2(7, 7, 3, 1, 0),
     FV2(7, 7, 3, 2, 0), FV2(1, 1, 1, 0, 0), FV2(1, 1, 1, 1, 0), FV2(1, 1, 1, 2, 0), FV2(1, 1, 2, 0, 0),
     FV2(1, 1, 2, 1, 0), FV2(1, 1, 2, 2, 0), FV2(1, 1, 3, 0, 0), FV2(1, 1, 3, 1, 0), FV2(1, 1, 3, 2, 0),
 };
-#undef FQ2
 #undef FQ
 #undef FV2
 #undef FV
-// rows_max: 128 admits the two-tile kernels (preferred), 64 only the one-tile ones
-int fused_variant(int T, int TD, int K, int act, bool hv, bool x3, int rows_max = P3_ROWS) {
-  for (int i = 0; i < (int)(sizeof(kFused) / sizeof(kFused[0])); ++i)
-    if (kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv &&
-        kFused[i].x3 == (int)x3 && kFused[i].rows <= rows_max)
-      return i;
-  return -1;
+constexpr int kNumFused = (int)(sizeof(kFused) / sizeof(kFused[0]));
+// the variant for a network: rows_max 128 admits the two-tile kernels
+// (preferred when admitted), 64 only the others; adot selects between the
+// register and the memory adot form where both exist
+// (the width-256 FC kernels are opt-in until measured: DBSDE_W256=1)
+int fused_variant(int T, int TD, int K, int act, bool hv, bool x3, int rows_max = P3_ROWS, bool adot = false) {
+  const char* ew = getenv("DBSDE_W256");
+  const bool wide = ew && ew[0] == '1';
+  int any = -1;
+  for (int i = 0; i < kNumFused; ++i)
+    if ((wide || kFused[i].T <= 8) && kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv &&
+        kFused[i].x3 == (int)x3 && kFused[i].rows <= rows_max) {
+      if (kFused[i].adot == (int)adot) return i;
+      if (any < 0) any = i;
+    }
+  return any;
 }
 
 // ---------------------------------------------------------------------------
@@ -412,9 +427,14 @@ int build_net(dbsde_ctx* c) {
   const bool want_x3 = !(ex3 && ex3[0] == '0');
   const char* ent = getenv("DBSDE_NT");
   c->nt2 = ent && ent[0] == '2';
+  const char* ead = getenv("DBSDE_ADOT");
+  c->adot = ead && ead[0] == '1';
   c->x3 = want_x3 && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, true) >= 0;
   c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3) >= 0;
   c->x3 = c->x3 && c->fused;
+  c->fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3, c->nt2 ? Q_ROWS : P3_ROWS,
+                                   c->adot)
+                   : -1;
   // FC / Resnet layouts the fused kernels do not cover: split-bf16 chain GEMMs
   // (uniform hidden width, output blocks a multiple of the column tile)
   c->x3chain = want_x3 && !c->fused && !c->has_v && uniform && c->Dp <= 128;
@@ -1413,6 +1433,7 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
   a.loss_part = c->loss_part;
   a.Hdot = c->Hdot;
   a.Alpha = c->Alpha;
+  a.Adot = c->Adot;
 
   // stage sequences (phase.hpp): every image streamed as two pieces, input
   // blocks [0, H) and [H, TI)
@@ -1440,7 +1461,7 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
   auto addC = [&](const float* img, int TO, int TI) { add(a.simgC, a.snfC, a.nC, img, TO, TI); };
   addA(c->imgX[0], TW, TDp);
   addC(c->imgX[0], TW, TDp);
-  const bool xfirst = c->x3 && c->has_v;   // phase C's X-first stage order (phase.hpp)
+  const bool xfirst = c->fv >= 0 && kFused[c->fv].xfirst;   // phase C's X-first stage order (phase.hpp)
   if (xfirst)
     for (int j = 1; j <= K; ++j) addC(c->imgX[j], TW, TDp);
   for (int j = 1; j <= K; ++j) {
@@ -1816,8 +1837,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   int nloss_parts;
   bool tnw_piped = false;
   FusedArgs fa;
-  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, K, c->act, c->has_v, c->x3,
-                                          c->nt2 ? Q_ROWS : P3_ROWS) : -1;
+  const int fv = c->fv;
   if (fv >= 0) {
     fa = fused_args(c, R, Rp, N1, q3);
     if (!fused_piece_counts_ok(c, fa)) return fail(c, DBSDE_EINVAL, "internal: fused kernel piece counts");
@@ -2091,8 +2111,7 @@ int dbsde_net_u_vjp(dbsde_ctx* c, const float* params, int R, const float* t, co
   const unsigned nb = (unsigned)((n + 255) / 256);
   RUN(c, "netu_input", 0.0, 0.0, netu_input_kernel<<<nb, 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
   if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
-  const int fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3,
-                                          c->nt2 ? Q_ROWS : P3_ROWS) : -1;
+  const int fv = c->fv;
   if (fv >= 0) {
     // ubar -> rres rows, zbar -> the sdw rows phase C reads (phase A's use of
     // sdw only feeds the residual row sums, unused here)

@@ -95,9 +95,11 @@ __device__ __forceinline__ void glds16(const float* g, floatx4* l) {
 }
 // s_waitcnt vmcnt(N) (expcnt / lgkmcnt untouched): vector-memory operations
 // complete in issue order, so this waits for everything but the N youngest
-template <int N>
+// (N is clamped to the 6-bit field: waiting for more than asked is safe)
+template <int N0>
 __device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  static_assert(N0 >= 0, "vmcnt count");
+  constexpr int N = N0 < 63 ? N0 : 63;
   __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
 }
 // workgroup barrier WITHOUT __syncthreads()'s release fence: that fence emits

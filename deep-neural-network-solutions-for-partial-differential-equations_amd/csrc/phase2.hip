@@ -9,10 +9,12 @@
 
 namespace dbsde {
 
-// stager of the two-tile kernels (split-bf16 pieces of 3 T fragments, T == TD)
-template <int T, int K, bool HV, int PH>
-using PieceStager2 = PieceStagerT<Q_NBUF, (3 * T) / P3_WAVES, 3 * T,
-                                  ((T + 1) / 2) * (PH == 0 ? 2 + 2 * K * (HV ? 2 : 1) : 1 + K * (HV ? 3 : 2))>;
+// stager: split-bf16 pieces; T == TD: every piece 3 T fragments (compile-time
+// piece count and a per-lane pointer table), else the runtime piece tables
+template <int T, int TD, int K, bool HV, int PH, int NBUF>
+using PieceStager2 = PieceStagerT<NBUF, (3 * (T < TD ? T : TD)) / P3_WAVES, T == TD ? 3 * T : 0,
+                                  T == TD ? ((T + 1) / 2) * (PH == 0 ? 2 + 2 * K * (HV ? 2 : 1) : 1 + K * (HV ? 3 : 2))
+                                          : 0>;
 
 // acc[t][o] += W(o, kb) . b[t](kb) over one piece for the NT tiles: per
 // fragment o the next fragment's three ds_read_b128 first, then the 6 NT
@@ -100,16 +102,16 @@ __device__ __forceinline__ void zero_nt(Mat<TT> (&m)[NT]) {
 // phase A, two tiles per wave: forward + input gradient + Z (+ residual row
 // sums).  Stage images as phaseA_kernel.
 // ---------------------------------------------------------------------------
-template <int T, int K, int ACT, bool HV>
+template <int T, int TD, int K, int ACT, bool HV, int NT, int NBUF, bool ADOT>
 __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p) {
-  constexpr int NT = Q_NT, TD = T, BUF = 3 * T * 64;
-  __shared__ floatx4 wl[Q_NBUF * BUF];
+  constexpr int TB = T > TD ? T : TD, BUF = 3 * TB * 64, ROWS = 16 * NT * P3_WAVES;
+  __shared__ floatx4 wl[NBUF * BUF];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int tile = blockIdx.x + p.tile0;   // 128-row tile (chunked launches offset it)
-  const int row0 = tile * Q_ROWS + wave * 16 * NT;   // register tile t: rows row0 + 16 t ..
+  const int tile = blockIdx.x + p.tile0;   // ROWS-row tile (chunked launches offset it)
+  const int row0 = tile * ROWS + wave * 16 * NT;   // register tile t: rows row0 + 16 t ..
   const int S = p.S, Wd = p.W;
-  PieceStager2<T, K, HV, 0> sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
+  PieceStager2<T, TD, K, HV, 0, NBUF> sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
   sg.start();
   Mat<TD> x[NT];
 #pragma unroll
@@ -289,18 +291,18 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p) 
 // reverse over (primal, tangent).  Stage images as phaseC_kernel (X-first
 // order for the x-stack networks).
 // ---------------------------------------------------------------------------
-template <int T, int K, int ACT, bool HV>
+template <int T, int TD, int K, int ACT, bool HV, int NT, int NBUF, bool ADOT>
 __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) {
-  constexpr int NT = Q_NT, TD = T, BUF = 3 * T * 64;
+  constexpr int TB = T > TD ? T : TD, BUF = 3 * TB * 64, ROWS = 16 * NT * P3_WAVES;
   // one __shared__ array (the loss slots after the ring): see phaseC_kernel
-  __shared__ floatx4 wl[Q_NBUF * BUF + P3_WAVES / 2];
-  double* lsum = (double*)(wl + Q_NBUF * BUF);
+  __shared__ floatx4 wl[NBUF * BUF + P3_WAVES / 2];
+  double* lsum = (double*)(wl + NBUF * BUF);
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int tile = blockIdx.x + p.tile0;
-  const int row0 = tile * Q_ROWS + wave * 16 * NT;
+  const int row0 = tile * ROWS + wave * 16 * NT;
   const int S = p.S, Wd = p.W;
-  PieceStager2<T, K, HV, 1> sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
+  PieceStager2<T, TD, K, HV, 1, NBUF> sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
   sg.start();
 
   // ---- residuals and closed-form cotangents of rows (row0 + 16 t + cl)
@@ -351,9 +353,12 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
   }
   if (lane == 0) lsum[wave] = lv;
 
-  Mat<T> ad[K + 1][NT];   // adot_j
+  // adot_j: all levels in registers, or (ADOT) the current level only, with
+  // every level stored to Adot for the reverse
+  constexpr int NAD = ADOT ? 1 : K + 1;
+  Mat<T> ad[NAD][NT];
   Mat<T> hd[NT], av[NT];
-  constexpr bool XFIRST = HV;
+  constexpr bool XFIRST = HV && !ADOT;
   zero_nt(ad[0]);
   stage_nt<T, TD, NT * TD, NT * T, NT>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -384,22 +389,30 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
       for (int rr = 0; rr < 4; ++rr) hd[t].v[o][rr] = act_1<ACT>(av[t].v[o][rr]) * ad[0][t].v[o][rr];
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
-    if constexpr (!XFIRST) zero_nt(ad[j]);
-    stage_nt<T, T, 0, 2 * NT * T, NT>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
+    constexpr int ja = ADOT ? 0 : j;
+    if constexpr (ADOT) {
+      // this level's accumulators reuse the registers of the previous one
+#pragma unroll
+      for (int t = 0; t < NT; ++t) fstore(ad[0][t], p.Adot, S, row0 + 16 * t, (j - 1) * Wd);
+    }
+    if constexpr (!XFIRST) zero_nt(ad[ja]);
+    constexpr int NAF = 2 * NT * T;   // (ADOT: the Adot stores are older, not counted)
+    stage_nt<T, T, 0, NAF, NT>(ad[ja], hd, sg, lane, [&]() __attribute__((always_inline)) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) bstore_stream(hd[t], p.Hdot, S, row0 + 16 * t, (j - 1) * Wd);
 #pragma unroll
       for (int t = 0; t < NT; ++t) fload(av[t], p.Abuf, S, row0 + 16 * t, j * Wd);
     });
-    if constexpr (HV && !XFIRST) stage_nt<T, TD, 0, 0, NT>(ad[j], zb, sg, lane, NoOp{});
+    if constexpr (HV && !XFIRST) stage_nt<T, TD, 0, 0, NT>(ad[ja], zb, sg, lane, NoOp{});
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int o = 0; o < T; ++o)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr)
-          hd[t].v[o][rr] = act_1<ACT>(av[t].v[o][rr]) * ad[j][t].v[o][rr] + p.rho * hd[t].v[o][rr];
+          hd[t].v[o][rr] = act_1<ACT>(av[t].v[o][rr]) * ad[ja][t].v[o][rr] + p.rho * hd[t].v[o][rr];
   });
+  constexpr int jK = ADOT ? 0 : K;   // ad[jK] = adot_K
   // reverse: p_{K+1} = ubar w_out ; alpha_K = w_out (ubar act'(a_K) + adot_K act''(a_K))
   Mat<T> pv[NT], al[NT];
 #pragma unroll
@@ -414,13 +427,14 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
         float d1, d2;
         act_12<ACT>(av[t].v[o][rr], d1, d2);
         pv[t].v[o][rr] = ub * wo[rr];
-        al[t].v[o][rr] = wo[rr] * (ub * d1 + ad[K][t].v[o][rr] * d2);
+        al[t].v[o][rr] = wo[rr] * (ub * d1 + ad[jK][t].v[o][rr] * d2);
       }
     }
   }
   SFor<0, K>::run([&](auto ic) __attribute__((always_inline)) {
     constexpr int j = K - decltype(ic)::value;
     Mat<T> gg[NT];
+    Mat<T> adr[ADOT ? NT : 1];   // ADOT: adot_{j-1} reloaded
     // p_j = rho p_{j+1} + alpha_j B_j, accumulated in place (rho is 0 or 1)
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -428,13 +442,15 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
       for (int o = 0; o < T; ++o)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) pv[t].v[o][rr] *= p.rho;
-    stage_nt<T, T, 0, 3 * NT * T, NT>(pv, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
+    constexpr int NAF = (ADOT ? 4 : 3) * NT * T;
+    stage_nt<T, T, 0, NAF, NT>(pv, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
 #pragma unroll
       for (int t = 0; t < NT; ++t) bstore_stream(al[t], p.Alpha, S, row0 + 16 * t, j * Wd);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         fload(av[t], p.Abuf, S, row0 + 16 * t, (j - 1) * Wd);
         fload(gg[t], p.G, S, row0 + 16 * t, (j - 1) * Wd);
+        if constexpr (ADOT) fload(adr[t], p.Adot, S, row0 + 16 * t, (j - 1) * Wd);
       }
     });
 #pragma unroll
@@ -445,16 +461,17 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
         for (int rr = 0; rr < 4; ++rr) {
           float d1, d2;
           act_12<ACT>(av[t].v[o][rr], d1, d2);
-          al[t].v[o][rr] = pv[t].v[o][rr] * d1 + gg[t].v[o][rr] * ad[j - 1][t].v[o][rr] * d2;
+          const float a1 = ADOT ? adr[ADOT ? t : 0].v[o][rr] : ad[ADOT ? 0 : j - 1][t].v[o][rr];
+          al[t].v[o][rr] = pv[t].v[o][rr] * d1 + gg[t].v[o][rr] * a1 * d2;
         }
   });
 #pragma unroll
   for (int t = 0; t < NT; ++t) bstore_stream(al[t], p.Alpha, S, row0 + 16 * t, 0);
 }
 
-#define DBSDE_PHASE2_DEFINE(T, K, ACT, HV)                           \
-  template __global__ void phaseA2_kernel<T, K, ACT, HV>(FusedArgs); \
-  template __global__ void phaseC2_kernel<T, K, ACT, HV>(FusedArgs);
+#define DBSDE_PHASE2_DEFINE(T, TD, K, ACT, HV, NT, NBUF, ADOT)                           \
+  template __global__ void phaseA2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>(FusedArgs); \
+  template __global__ void phaseC2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>(FusedArgs);
 DBSDE_PHASE2_INSTANCES(DBSDE_PHASE2_DEFINE)
 #undef DBSDE_PHASE2_DEFINE
 

@@ -10,6 +10,10 @@
 // and each weight byte streamed from L2 serves 128 rows instead of 64.  The
 // ring is 4 pieces deep (3 in flight, 84 KiB).
 //
+// The same kernels with one tile per wave and 48 KiB pieces serve the FC
+// width-256 network of config 4 (hjb_implement.py:590-604), where one 16-row
+// tile already fills the register file (a level is 64 VGPRs per lane).
+//
 // Phase A keeps no act'(a_j) registers (they would need 224 per wave): the
 // backward reloads a_j from Abuf, which it wrote a few stages earlier, and
 // recomputes act'(a_j) -- the same reload phase C makes.
@@ -18,22 +22,34 @@
 
 namespace dbsde {
 
-constexpr int Q_NT = 2;                            // 16-row tiles per wave
-constexpr int Q_ROWS = 16 * Q_NT * P3_WAVES;       // rows per workgroup
-constexpr int Q_NBUF = 4;                          // split-bf16 weight ring depth
+constexpr int Q_NT = 2;                            // 16-row tiles per wave (width-112 kernels)
+constexpr int Q_ROWS = 16 * Q_NT * P3_WAVES;       // rows per workgroup of those
 
-template <int T, int K, int ACT, bool HV>
+// Template parameters of the phase2 kernels:
+//   T, TD   level / state width in 16-column blocks (T != TD: runtime piece
+//           tables, pieces of 3 TO fragments for the stage's TO)
+//   K, ACT, HV  as phase.hpp
+//   NT      16-row register tiles per wave (rows per workgroup 64 NT)
+//   NBUF    LDS ring depth in pieces of 3 max(T, TD) KiB
+//   ADOT    phase C keeps adot_j in memory (Adot, tile order) between the
+//           tangent and the reverse instead of registers (wide levels), and
+//           runs the x-stack products level by level (no X-first order)
+template <int T, int TD, int K, int ACT, bool HV, int NT, int NBUF, bool ADOT>
 __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p);
-template <int T, int K, int ACT, bool HV>
+template <int T, int TD, int K, int ACT, bool HV, int NT, int NBUF, bool ADOT>
 __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p);
 
 // the instantiations phase2.hip builds (its own translation unit, compiled in
-// parallel with engine.hip)
-#define DBSDE_PHASE2_INSTANCES(X) \
-  X(7, 3, 0, true) X(7, 3, 0, false) X(7, 3, 1, true) X(7, 3, 1, false) X(7, 3, 2, true) X(7, 3, 2, false)
-#define DBSDE_PHASE2_EXTERN(T, K, ACT, HV)                                  \
-  extern template __global__ void phaseA2_kernel<T, K, ACT, HV>(FusedArgs); \
-  extern template __global__ void phaseC2_kernel<T, K, ACT, HV>(FusedArgs);
+// parallel with engine.hip): the width-112 networks with two tiles per wave,
+// the adot-in-memory variants of them (A/B), and config 4's FC [101,256x4,1]
+#define DBSDE_PHASE2_INSTANCES(X)                                                                                 \
+  X(7, 7, 3, 0, true, 2, 4, false) X(7, 7, 3, 0, false, 2, 4, false) X(7, 7, 3, 1, true, 2, 4, false)            \
+  X(7, 7, 3, 1, false, 2, 4, false) X(7, 7, 3, 2, true, 2, 4, false) X(7, 7, 3, 2, false, 2, 4, false)           \
+  X(7, 7, 3, 0, true, 2, 4, true) X(7, 7, 3, 1, true, 2, 4, true) X(7, 7, 3, 2, true, 2, 4, true)                \
+  X(16, 7, 3, 0, false, 1, 3, true) X(16, 7, 3, 1, false, 1, 3, true) X(16, 7, 3, 2, false, 1, 3, true)
+#define DBSDE_PHASE2_EXTERN(T, TD, K, ACT, HV, NT, NBUF, ADOT)                                   \
+  extern template __global__ void phaseA2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>(FusedArgs); \
+  extern template __global__ void phaseC2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>(FusedArgs);
 DBSDE_PHASE2_INSTANCES(DBSDE_PHASE2_EXTERN)
 #undef DBSDE_PHASE2_EXTERN
 
