@@ -548,7 +548,12 @@ int build_buffers(dbsde_ctx* c) {
     }
   }
   const int fsplit = img_x3 ? 1 : 0;
-  auto frag = [fsplit](PackDesc d, float* img, int tin, int tout, int row0, int col0) {
+  // the fused phase kernels read only the fragment images: their contexts skip
+  // the fp32 copies the per-layer chain GEMMs use (half the pack writes, and
+  // all of its transposed ones)
+  const bool images_only = c->fused;
+  auto frag = [fsplit, images_only](PackDesc d, float* img, int tin, int tout, int row0, int col0) {
+    if (images_only) d.dst = nullptr;
     d.fdst = img;
     d.ftin = tin;
     d.ftout = tout;
@@ -897,6 +902,9 @@ int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
     if (ra.ldx > CP_SROW) return fail(c, DBSDE_EINVAL, "internal: correlated rollout row staging");
     RUN(c, name, 2.0 * steps * ra.nb * ra.nb / 2, bytes,
         launch_corr(ra, s));
+  } else if (ra.out == PATH_ROLLOUT && ra.ldx % 4 == 0) {
+    const int nthr = ra.M * (ra.ldx / 4);   // whole-row float4 stores
+    RUN(c, name, 0.0, bytes, rollout4_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
   } else {
     const int nthr = ra.M * ra.D;
     RUN(c, name, 0.0, bytes, rollout_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
@@ -999,10 +1007,12 @@ __device__ __forceinline__ void pack_block(const PackDesc* descs, int di, const 
       const double s2 = 0.0, s3 = 0.0;
       v = d.scale * (float)((s0 + s1) + (s2 + s3));
     }
-    if (d.transpose)
-      d.dst[(size_t)cc * d.dst_ld + r] = v;
-    else
-      d.dst[(size_t)r * d.dst_ld + cc] = v;
+    if (d.dst) {
+      if (d.transpose)
+        d.dst[(size_t)cc * d.dst_ld + r] = v;
+      else
+        d.dst[(size_t)r * d.dst_ld + cc] = v;
+    }
     if (d.fdst) {
       const int dr = (d.transpose ? cc : r) + d.frow0, dc = (d.transpose ? r : cc) + d.fcol0;
       if (d.fsplit) {

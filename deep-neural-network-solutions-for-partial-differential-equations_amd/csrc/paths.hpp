@@ -162,6 +162,84 @@ __global__ void __launch_bounds__(256) rollout_kernel(RolloutArgs p) {
   }
 }
 
+// The same rollout with whole-row float4 stores: thread per (path m, 16-byte
+// column group c of the xin / sdw rows), columns 4c .. 4c + 3 = t (column 0),
+// X_d (column 1 + d), 1 (column D + 1) and zero padding.  Every row is written
+// whole, 16 bytes per lane: the thread-per-dimension form leaves the padding
+// columns and the misaligned row ends to partial-line writes (the L2 then reads
+// the rest of each line back: 23 MB of reads for a kernel with no inputs,
+// profiles/r3_pmc_fetch).  Per dimension the arithmetic is rollout_kernel's,
+// so X is bit-identical.
+__global__ void __launch_bounds__(256) rollout4_kernel(RolloutArgs p) {
+  const int C = p.ldx >> 2;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= p.M * C) return;
+  const int m = gid / C, c = gid - m * C;
+  const int N1 = p.N + 1;
+  float x[4], w0[4];
+  bool live[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int d = 4 * c + k - 1;
+    live[k] = d >= 0 && d < p.D;
+    const int dd = live[k] ? d : 0;
+    x[k] = live[k] ? p.Xi[(p.xi_rows == 1 ? 0 : m) * p.D + dd] : 0.f;
+    w0[k] = (live[k] && p.W) ? p.W[(size_t)m * N1 * p.nb + dd] : 0.f;
+  }
+  const double dt64 = (double)p.T / (double)p.N;
+  const float sqdt = sqrtf(p.T / (float)p.N);
+  double tacc = 0.0;
+  float t0 = p.t ? p.t[(size_t)m * N1] : 0.0f;
+  size_t r = (size_t)m * N1;
+  for (int n0 = 0; n0 < p.N; n0 += 4) {
+    // increments of the live dimensions; every call sees the same grid sum, so
+    // t1 (the times of steps n0 + 1 .. n0 + 4) is the same from each
+    float dw[4][4], t1[4] = {0.f, 0.f, 0.f, 0.f};
+    double tn = tacc;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dw[k][i] = 0.f;
+      if (live[k]) {
+        tn = tacc;
+        step_block(p, m, 4 * c + k - 1, n0, w0[k], tn, dt64, sqdt, dw[k], t1);
+      }
+    }
+    tacc = tn;   // unchanged for a thread without live dimensions: its rows hold no t
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (n0 + i >= p.N) break;
+      const float dt = rn_sub(t1[i], t0);
+      floatx4 xo, so;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int col = 4 * c + k;
+        float sv = 0.f;
+        if (live[k]) {
+          const float sg = rn_add(rn_mul(p.sig_a, x[k]), p.sig_b);
+          sv = rn_mul(sg, dw[k][i]);
+        }
+        xo[k] = col == 0 ? t0 : (col == p.D + 1 ? 1.f : x[k]);
+        so[k] = sv;
+        if (live[k]) x[k] = rn_add(rn_add(x[k], rn_mul(rn_mul(p.mu_a, x[k]), dt)), sv);
+      }
+      *(floatx4*)(p.xin + r * p.ldx + 4 * c) = xo;
+      *(floatx4*)(p.sdw + r * p.ldx + 4 * c) = so;
+      t0 = t1[i];
+      ++r;
+    }
+  }
+  floatx4 xo, so;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {   // n = N
+    const int col = 4 * c + k;
+    xo[k] = col == 0 ? t0 : (col == p.D + 1 ? 1.f : x[k]);
+    so[k] = 0.f;
+  }
+  *(floatx4*)(p.xin + r * p.ldx + 4 * c) = xo;
+  *(floatx4*)(p.sdw + r * p.ldx + 4 * c) = so;
+}
+
 // --------------------------------------------------------------------------
 // Cholesky-correlated device mode (with_corr...py:339-341: dW = L (sqrt(dt) z))
 // with the correlation product on the matrix cores: per step n the increments

@@ -186,3 +186,43 @@ def test_fused_update_with_a_prefetched_rollout_beside_it(pkg, dev):
     torch.cuda.synchronize()
     for x, y in ((a.params, b.params), (oa["m"], ob["m"]), (oa["v"], ob["v"])):
         torch.testing.assert_close(x, y, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("name", ["g1_w256_hjb_FC_Sine_N20.npz"])
+def test_width256_fused_kernels_match_reference(pkg, dev, name):
+    """Config 4's FC-Sine [101,256x4,1] (hjb_implement.py:590-604) on the
+    fused width-256 phase kernels (phase2.hip, one 16-row tile per wave, adot
+    through memory; DBSDE_W256=1) against the reference fixture, tolerances as
+    test_gpu_parity."""
+    from test_gpu_parity import make_solver
+    g = _load(name)
+    old = os.environ.get("DBSDE_W256")
+    os.environ["DBSDE_W256"] = "1"
+    try:
+        s = make_solver(pkg, dev, g)
+    finally:
+        if old is None:
+            del os.environ["DBSDE_W256"]
+        else:
+            os.environ["DBSDE_W256"] = old
+    assert s.matrix_form & 1 and not s.matrix_form & 4, "expected the fused split-bf16 kernels"
+    layers = [int(v) for v in g["layers"]]
+    D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
+    params = torch.from_numpy(g["params"]).to(dev)
+    out = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (N + 1) * D, device=dev),
+               Y=torch.empty(M * (N + 1), device=dev), Z=torch.empty(M * (N + 1) * D, device=dev))
+    grad = torch.empty_like(params)
+    s.loss_grad(params, M, N, torch.from_numpy(g["Xi"]).to(dev).contiguous(),
+                t=torch.from_numpy(g["t"]).to(dev).reshape(M, N + 1).contiguous(),
+                W=torch.from_numpy(g["W"]).to(dev).contiguous(), grad=grad, **out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["X"].cpu().numpy().reshape(M, N + 1, D), g["X"])
+    np.testing.assert_allclose(float(out["loss"]), float(g["loss"]), rtol=1e-4)
+    Y = out["Y"].cpu().numpy().reshape(M, N + 1, 1)
+    np.testing.assert_allclose(Y, g["Y"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Y"]).max()))
+    if "Z" in g:
+        Z = out["Z"].cpu().numpy().reshape(M, N + 1, D)
+        np.testing.assert_allclose(Z, g["Z"], rtol=0, atol=1e-4 * max(1.0, np.abs(g["Z"]).max()))
+    used = g["used"]
+    r = grad.cpu().numpy()
+    np.testing.assert_allclose(r[used], g["grad"][used], rtol=0, atol=2e-4 * np.abs(g["grad"]).max())
