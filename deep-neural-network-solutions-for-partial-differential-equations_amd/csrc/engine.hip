@@ -162,6 +162,7 @@ struct dbsde_ctx {
   bool adot = false;              // ... phase C with adot in memory where both forms exist (DBSDE_ADOT=1)
   int fv = -1;                    // the fused variant (kFused index) or -1
   bool x3chain = false;           // per-layer chain GEMMs in split-bf16 form (chainx3.hpp)
+  bool tnx3 = false;              // the split-K weight-gradient tiles in split-bf16 form (tnx3.hpp; !tnw layouts)
   // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
   // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
   std::vector<float*> imgX, imgZ, imgF, imgB;
@@ -314,10 +315,10 @@ constexpr int kNumFused = (int)(sizeof(kFused) / sizeof(kFused[0]));
 // the variant for a network: rows_max 128 admits the two-tile kernels
 // (preferred when admitted), 64 only the others; adot selects between the
 // register and the memory adot form where both exist
-// (the width-256 FC kernels are opt-in until measured: DBSDE_W256=1)
+// (DBSDE_W256=0 leaves the width-256 FC networks to the per-layer chain)
 int fused_variant(int T, int TD, int K, int act, bool hv, bool x3, int rows_max = P3_ROWS, bool adot = false) {
   const char* ew = getenv("DBSDE_W256");
-  const bool wide = ew && ew[0] == '1';
+  const bool wide = !(ew && ew[0] == '0');
   int any = -1;
   for (int i = 0; i < kNumFused; ++i)
     if ((wide || kFused[i].T <= 8) && kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv &&
@@ -437,8 +438,11 @@ int build_net(dbsde_ctx* c) {
                    : -1;
   // FC / Resnet layouts the fused kernels do not cover: split-bf16 chain GEMMs
   // (uniform hidden width, output blocks a multiple of the column tile)
-  c->x3chain = want_x3 && !c->fused && !c->has_v && uniform && c->Dp <= 128;
-  for (int j = 0; j <= c->K && c->x3chain; ++j) c->x3chain = (c->Wp[j] / 16) % nt_for(c->Wp[j]) == 0;
+  // (the same layouts' weight-gradient tiles run split-bf16 behind the fused
+  // phase kernels too: tnx3)
+  c->tnx3 = want_x3 && !c->has_v && uniform && c->Dp <= 128;
+  for (int j = 0; j <= c->K && c->tnx3; ++j) c->tnx3 = (c->Wp[j] / 16) % nt_for(c->Wp[j]) == 0;
+  c->x3chain = c->tnx3 && !c->fused;
   // problem kind: Brownian dimension, g columns, u clamp
   const dbsde_problem& pr = g.problem;
   if (pr.kind != DBSDE_PROB_DIAG && pr.kind != DBSDE_PROB_HESTON) return fail(c, DBSDE_EINVAL, "unknown problem kind");
@@ -1513,7 +1517,7 @@ int dbsde_matrix_form(const dbsde_ctx* c) {
   if (!c) return 0;
   // bit 1: the wave-tile weight-gradient kernel in split-bf16 form, or the
   // chain layouts' weight-gradient tiles (tnx3.hpp, split-bf16 with x3chain)
-  const bool tn_x3 = c->tnw ? c->tnw_x3 : c->x3chain;
+  const bool tn_x3 = c->tnw ? c->tnw_x3 : c->tnx3;
   return (c->x3 ? 1 : 0) | (tn_x3 ? 2 : 0) | (c->x3chain ? 4 : 0);
 }
 
@@ -1792,7 +1796,7 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
     tfl += 2.0 * 2.0 * R * (L[K + 1] + 1);
   }
   if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
-  if (c->x3chain) {
+  if (c->tnx3) {
     // split-bf16 tiles for the layer problems (tnx3.hpp), the fp32 kernel
     // for the one-row output layer
     int maxt3 = 0;
@@ -1984,7 +1988,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     const long long n = (long long)R * D;
     RUN(c, "export", 0.0, 0.0,
         export_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, out->X,
-                                                                  out->Y, out->Z));
+                                                                  out->Y, out->Z, nullptr));
   }
   if ((rc = join_side(c, 1))) return rc;
   return DBSDE_OK;
@@ -2086,8 +2090,15 @@ int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const 
   RUN(c, "netu_input", 0.0, 0.0,
       netu_input_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
   if (Rp > R) HIPC(c, hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, s));
-  if ((rc = forward_and_inputgrad(c, R, Rp, true))) return rc;
-  {
+  if (c->fv >= 0) {
+    // the fused forward + input-gradient kernel writes u and Z (its residual
+    // row sums read sdw, unused here)
+    FusedArgs fa = fused_args(c, R, Rp, 1, false);
+    if (!fused_piece_counts_ok(c, fa)) return fail(c, DBSDE_EINVAL, "internal: fused kernel piece counts");
+    const int WR = kFused[c->fv].rows;
+    RUN(c, "fused_fwd_inputgrad", 0.0, 0.0, kFused[c->fv].A<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));
+  } else {
+    if ((rc = forward_and_inputgrad(c, R, Rp, true))) return rc;
     ChainArgs a = base_args(c);
     zgemm_args(c, a);
     if ((rc = chain<EPI_STORE>(c, "gemm_z", a, Rp, c->Dp, c->Dp / 16, zgemm_flops(c, R), 0.0))) return rc;
@@ -2095,7 +2106,7 @@ int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const 
   const long long m = (long long)R * D;
   RUN(c, "export", 0.0, 0.0,
       export_kernel<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, nullptr, u,
-                                                                Du));
+                                                                Du, (c->fv < 0 && c->u_clamp) ? c->umask : nullptr));
   return DBSDE_OK;
 }
 

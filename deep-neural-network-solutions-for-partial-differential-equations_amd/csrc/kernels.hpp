@@ -863,14 +863,17 @@ __device__ __forceinline__ void fused_opt_prologue(FusedOpt& fo, bool step_write
 // output export: rows -> reference layouts
 // --------------------------------------------------------------------------
 #ifndef DBSDE_DEVICE_HELPERS_ONLY
+// zmask (nullable): the u-clamp gradient mask (heston_dnnpde.py:568) for a
+// Z that is not masked yet (the per-layer net_u's plain Z GEMM)
 __global__ void __launch_bounds__(256) export_kernel(const float* xin, const float* zfull, int ldx, const float* u,
-                                                     int R, int D, float* X, float* Y, float* Z) {
+                                                     int R, int D, float* X, float* Y, float* Z,
+                                                     const float* zmask) {
   const long long i = blockIdx.x * 256LL + threadIdx.x;
   if (i >= (long long)R * D) return;
   const long long r = i / D;
   const int d = (int)(i - r * D);
   if (X) X[i] = xin[r * ldx + 1 + d];
-  if (Z) Z[i] = zfull[r * ldx + 1 + d];
+  if (Z) Z[i] = zmask ? zfull[r * ldx + 1 + d] * zmask[r] : zfull[r * ldx + 1 + d];
   if (Y && d == 0) Y[r] = u[r];
 }
 #endif

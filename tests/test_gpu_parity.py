@@ -57,7 +57,7 @@ def dev():
     return torch.device("cuda:0")
 
 
-def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=2):
+def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=1):
     """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at
     create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0); x3=False
     the fp32-input MFMA form of the fused phase and weight-gradient kernels
@@ -81,7 +81,7 @@ def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=2):
                 os.environ[k] = v
 
 
-def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, nt=2):
+def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, nt=1):
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
     s = make_solver(pkg, dev, g, fused, x3=x3, nt=nt)
@@ -103,16 +103,14 @@ def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, nt=2):
     return res
 
 
-@pytest.mark.parametrize("fused", ["fused", "fused_nt1", "fused_fp32", "chain"])
+@pytest.mark.parametrize("fused", ["fused", "fused_fp32", "chain"])
 @pytest.mark.parametrize("path", G1, ids=[os.path.basename(p)[3:-4] for p in G1])
 def test_loss_grad_matches_reference(pkg, dev, path, fused):
     """fused: the default fused kernels (split-bf16 matrix form at width
-    110/112, two 16-row tiles per wave); fused_nt1: the same with one tile
-    per wave; fused_fp32: the fused kernels on fp32-input MFMA; chain: the
-    per-layer GEMM path."""
+    110/112 and, for FC, 256); fused_fp32: the fused kernels on fp32-input
+    MFMA; chain: the per-layer GEMM path."""
     g = _load(path)
-    r = native_case(pkg, dev, g, fused=fused != "chain", x3=fused in ("fused", "fused_nt1"),
-                    nt=1 if fused == "fused_nt1" else 2)
+    r = native_case(pkg, dev, g, fused=fused != "chain", x3=fused == "fused")
     if str(g["problem"]) == "heston":
         # the reference's torch.sqrt on the CPU is MKL vsSqrt (ATen vml), which
         # is not correctly rounded at near-ties; the kernel's sqrt is (as numpy's,

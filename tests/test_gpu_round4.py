@@ -91,8 +91,8 @@ def test_loss_function_backward_fills_grad(pkg, dev, fixture, cls, mode):
     assert not l2.requires_grad
 
 
-@pytest.mark.parametrize("k,layers_h,act", [(1, 4 * [16], "Tanh"), (3, 4 * [110], "Sine")],
-                         ids=["k1_w16_fp32", "k3_w110_x3"])
+@pytest.mark.parametrize("k,layers_h,act", [(1, 4 * [16], "Tanh"), (3, 4 * [110], "Sine"), (50, 4 * [110], "Sine")],
+                         ids=["k1_w16_fused_fp32", "k3_w110_chain", "k50_w110_fused_x3"])
 def test_heston_net_u_backward_through_the_clamp(pkg, dev, k, layers_h, act):
     """heston_dnnpde.py:560-579: u = max(net, 0); the backward of (u, Du)
     passes only where net >= 0.  The output bias is set to the median of the
@@ -192,8 +192,8 @@ def test_fused_update_with_a_prefetched_rollout_beside_it(pkg, dev):
 def test_width256_fused_kernels_match_reference(pkg, dev, name):
     """Config 4's FC-Sine [101,256x4,1] (hjb_implement.py:590-604) on the
     fused width-256 phase kernels (phase2.hip, one 16-row tile per wave, adot
-    through memory; DBSDE_W256=1) against the reference fixture, tolerances as
-    test_gpu_parity."""
+    through memory; the default, DBSDE_W256=1 made explicit) against the
+    reference fixture, tolerances as test_gpu_parity."""
     from test_gpu_parity import make_solver
     g = _load(name)
     old = os.environ.get("DBSDE_W256")
