@@ -89,9 +89,14 @@ __device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int
   for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 16 * t));
 }
 
+// The LDS destination as a local-address-space pointer built from the low
+// half of the generic address (the LDS offset; the aperture sits in the high
+// half): the plain generic -> local cast carries a null check (s_cselect of
+// src_shared_base per issue) that some register assignments cannot even encode.
 __device__ __forceinline__ void glds16(const float* g, floatx4* l) {
+  const unsigned off = (unsigned)(uintptr_t)l;
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+                                   (__attribute__((address_space(3))) void*)(uintptr_t)off, 16, 0, 0);
 }
 // s_waitcnt vmcnt(N) (expcnt / lgkmcnt untouched): vector-memory operations
 // complete in issue order, so this waits for everything but the N youngest
@@ -393,6 +398,78 @@ __device__ __forceinline__ void sgemm_x3_piece(Mat<TO>& acc, const Split3& s, co
     __builtin_amdgcn_sched_barrier(0);
   });
 }
+// The same piece with the MFMA chains of two fragments interleaved: one
+// scheduling region per fragment pair (o0, o1), its twelve MFMAs alternating
+// between the two accumulators, the next pair's six ds_read_b128 issued at
+// the region's top (48 VGPRs of weight operands instead of 24).  A chain of
+// six dependent v_mfma_f32_16x16x32_bf16 on one accumulator does not issue
+// back to back; two interleaved chains do (tools/ubench/piece_x3.hip).
+template <int TO, int TI, int KBN>
+__device__ __forceinline__ void sgemm_x3_piece_pairs(Mat<TO>& acc, const Split3& s, const floatx4* img, int lane,
+                                                     const Mat<TI>& b, uintx4 (&sn)[3]) {
+  constexpr bool NEXT = KBN < (TI + 1) / 2;
+  constexpr int NPR = (TO + 1) / 2;
+  const uintx4* im = (const uintx4*)img;
+  uintx4 w[2][2][3];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      if (k < TO) w[0][k][p] = im[(3 * k + p) * 64 + lane];
+  __builtin_amdgcn_sched_barrier(0);
+  SFor<0, NPR>::run([&](auto gc) __attribute__((always_inline)) {
+    constexpr int g = decltype(gc)::value;
+    constexpr int o0 = 2 * g, o1 = 2 * g + 1;
+    constexpr bool two = o1 < TO;
+    constexpr int nrd = g + 1 < NPR ? 3 * ((2 * (g + 1) + 1 < TO) ? 2 : 1) : 0;   // next pair's reads
+    if constexpr (g + 1 < NPR) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          if (2 * (g + 1) + k < TO) w[(g + 1) & 1][k][p] = im[(3 * (2 * (g + 1) + k) + p) * 64 + lane];
+    }
+    // the split of the next input block, one dword pair per region (4 pairs)
+    if constexpr (NEXT && g < 4) split_pair<TI, NEXT ? KBN : 0, g>(b, sn[0], sn[1], sn[2]);
+    if constexpr (NEXT && NPR < 4 && g == NPR - 1) {   // fewer regions than pairs: the rest here
+      SFor<NPR, 4>::run([&](auto dc) __attribute__((always_inline)) {
+        split_pair<TI, NEXT ? KBN : 0, decltype(dc)::value>(b, sn[0], sn[1], sn[2]);
+      });
+    }
+    const uintx4* wa = w[g & 1][0];
+    const uintx4* wb = w[g & 1][1];
+    floatx4 a = acc.v[o0], c = acc.v[two ? o1 : o0];
+    a = mfma_bf(wa[0], s.l, a);
+    if constexpr (two) c = mfma_bf(wb[0], s.l, c);
+    a = mfma_bf(wa[0], s.m, a);
+    if constexpr (two) c = mfma_bf(wb[0], s.m, c);
+    a = mfma_bf(wa[1], s.m, a);
+    if constexpr (two) c = mfma_bf(wb[1], s.m, c);
+    a = mfma_bf(wa[1], s.h, a);
+    if constexpr (two) c = mfma_bf(wb[1], s.h, c);
+    a = mfma_bf(wa[2], s.h, a);
+    if constexpr (two) c = mfma_bf(wb[2], s.h, c);
+    acc.v[o0] = mfma_bf(wa[0], s.h, a);
+    if constexpr (two) acc.v[o1] = mfma_bf(wb[0], s.h, c);
+    if constexpr (nrd > 0) __builtin_amdgcn_sched_group_barrier(0x100, nrd, 0);   // DS read
+#pragma unroll
+    for (int k = 0; k < (two ? 12 : 6); ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // VALU
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+// piece kind: 0 = sgemm_x3_piece (one chain at a time), 1 = fragment pairs
+#ifndef DBSDE_PIECE_PAIRS
+#define DBSDE_PIECE_PAIRS 0
+#endif
+// phase A: act'(a_j) recomputed from Abuf in the backward (1) or kept (0)
+#ifndef DBSDE_A_RECOMP
+#define DBSDE_A_RECOMP 0
+#endif
+
 template <int TO, int TI, int NPRE, int NAFTER, int KB, bool PF, class SG, class F>
 __device__ __forceinline__ void stage_x3_from(Mat<TO>& acc, const Mat<TI>& b, SG& sg, int lane, F&& after,
                                               const Split3& s) {
@@ -404,7 +481,10 @@ __device__ __forceinline__ void stage_x3_from(Mat<TO>& acc, const Mat<TI>& b, SG
       __builtin_amdgcn_sched_barrier(0);
     }
     uintx4 sn[3];
-    sgemm_x3_piece<TO, TI, KB + 1, PF>(acc, s, w, lane, b, sn);
+    if constexpr (DBSDE_PIECE_PAIRS && PF)
+      sgemm_x3_piece_pairs<TO, TI, KB + 1>(acc, s, w, lane, b, sn);
+    else
+      sgemm_x3_piece<TO, TI, KB + 1, PF>(acc, s, w, lane, b, sn);
     sg.mark();
     if constexpr (KB + 1 < NKB)
       stage_x3_from<TO, TI, NPRE, NAFTER, KB + 1, PF>(
@@ -458,7 +538,10 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
   Mat<TD> x;
   bload(x, p.xin, p.Dp, row0, 0);
 
-  Mat<T> s1[K + 1];   // act'(a_j)
+  // act'(a_j) in registers, or (RECOMP, DBSDE_A_RECOMP) recomputed in the
+  // backward from a_j reloaded out of Abuf (frees 3 T registers x 4 levels)
+  constexpr bool RECOMP = DBSDE_A_RECOMP != 0;
+  Mat<T> s1[RECOMP ? 1 : K + 1];
   Mat<T> h, acc;
   zero(acc);
   stage_mm<X3, T, TD, TD, 0, PFA>(acc, x, sg, lane, NoOp{});
@@ -470,7 +553,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
       float f, d;
       act_v1<ACT>(acc.v[o][r], f, d);
       h.v[o][r] = f;
-      s1[0].v[o][r] = d;
+      if constexpr (!RECOMP) s1[0].v[o][r] = d;
     }
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
@@ -492,7 +575,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
       for (int r = 0; r < 4; ++r) {
         float f, d;
         act_v1<ACT>(acc.v[o][r], f, d);
-        s1[j].v[o][r] = d;
+        if constexpr (!RECOMP) s1[j].v[o][r] = d;
         h.v[o][r] = f + p.rho * h.v[o][r];
       }
   });
@@ -525,20 +608,23 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       g.v[o][r] = wo[r];
-      dl.v[o][r] = wo[r] * s1[K].v[o][r];
+      // (acc still holds a_K)
+      dl.v[o][r] = wo[r] * (RECOMP ? act_1<ACT>(acc.v[o][r]) : s1[RECOMP ? 0 : K].v[o][r]);
     }
   }
   Mat<TD> z;
   zero(z);
+  Mat<T> av;   // RECOMP: a_{j-1}, reloaded
   SFor<0, K>::run([&](auto ic) __attribute__((always_inline)) {
     constexpr int j = K - decltype(ic)::value;
     auto prev = [&]() __attribute__((always_inline)) {   // (g_j, delta_j) of the previous step
       if constexpr (j < K) fstore(g, p.G, S, row0, j * Wd);
       bstore_stream(dl, p.Delta, S, row0, j * Wd);
+      if constexpr (RECOMP) fload(av, p.Abuf, S, row0, (j - 1) * Wd);
     };
     Mat<T> gn;
     zero(gn);
-    constexpr int NPREV = j < K ? 2 * T : T;
+    constexpr int NPREV = (j < K ? 2 * T : T) + (RECOMP ? T : 0);
     if constexpr (HV) {
       stage_mm<X3, TD, T, 0, NPREV, PFA>(z, dl, sg, lane, prev);   // Z += delta_j V_j
       stage_mm<X3, T, T, 0, 0, PFA>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
@@ -551,7 +637,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
       for (int r = 0; r < 4; ++r) {
         const float gv = gn.v[o][r] + p.rho * g.v[o][r];
         g.v[o][r] = gv;
-        dl.v[o][r] = gv * s1[j - 1].v[o][r];
+        dl.v[o][r] = gv * (RECOMP ? act_1<ACT>(av.v[o][r]) : s1[RECOMP ? 0 : j - 1].v[o][r]);
       }
   });
   stage_mm<X3, TD, T, 0, 2 * T + TD, PFA>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in

@@ -146,6 +146,42 @@ __device__ __forceinline__ void one_piece(Mat<7>& acc, const Split3& s, const fl
   }
 }
 
+// mode 6/7: the phase kernels' piece pipeline -- PieceStager (3-buffer LDS
+// ring, LDS-DMA of each piece two ahead from a 56-piece image in global memory
+// (L2 resident), counted vmcnt wait + barrier per piece) around
+// sgemm_x3_piece (6) or the pairs piece (7)
+template <int MODE, int WPS>
+__global__ void __launch_bounds__(256, WPS) kern_staged(float* out, const float* const* pieces, int iters) {
+  constexpr int BUF = 3 * 7 * 64;
+  __shared__ floatx4 wl[P3_NBUF_X3 * BUF];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  Mat<7> b, acc;
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    b.v[t] = floatx4{1.f, 0.5f, 0.25f, 0.125f} * (float)(lane + t + 1) * 1.0001f;
+    acc.v[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  Split3 s = split_block<7, 0>(b);
+  for (int it = 0; it < iters; ++it) {
+    PieceStagerT<P3_NBUF_X3, 5, 21, 56> sg{wl, pieces, nullptr, 56, 0, wave, lane, BUF};
+    sg.start();
+    SFor<0, 56>::run([&](auto kc) __attribute__((always_inline)) {
+      const floatx4* w = sg.template next<0>();
+      uintx4 sn[3];
+      if constexpr (MODE == 6)
+        sgemm_x3_piece<7, 7, 1, true>(acc, s, w, lane, b, sn);
+      else
+        sgemm_x3_piece_pairs<7, 7, 1>(acc, s, w, lane, b, sn);
+      s = Split3{__builtin_bit_cast(bf16x8, sn[0]), __builtin_bit_cast(bf16x8, sn[1]), __builtin_bit_cast(bf16x8, sn[2])};
+    });
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < 7; ++t) sum += acc.v[t][0] + acc.v[t][1] + acc.v[t][2] + acc.v[t][3];
+  out[blockIdx.x * 256 + threadIdx.x] = sum;
+}
+
 template <int MODE, int WPS>
 __global__ void __launch_bounds__(256, WPS) kern(float* out, int iters) {
   __shared__ floatx4 wl[3 * 7 * 64];
@@ -203,7 +239,47 @@ void run(const char* name) {
   (void)hipFree(out);
 }
 
+template <int MODE, int WPS>
+void run_staged(const char* name, int blocks_per_cu_x) {
+  const int blocks = 256 * WPS * blocks_per_cu_x / 2, iters = 40;
+  float* out;
+  (void)hipMalloc(&out, blocks * 256 * 4);
+  float* img;
+  (void)hipMalloc(&img, 56 * 21 * 1024);
+  (void)hipMemset(img, 0x3f, 56 * 21 * 1024);
+  const float* h[64];
+  for (int k = 0; k < 64; ++k) h[k] = img + (size_t)(k % 56) * 21 * 256;
+  const float** dp;
+  (void)hipMalloc(&dp, sizeof(h));
+  (void)hipMemcpy(dp, h, sizeof(h), hipMemcpyHostToDevice);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  kern_staged<MODE, WPS><<<blocks, 256>>>(out, dp, iters);
+  float best = 1e30f;
+  for (int r = 0; r < 3; ++r) {
+    (void)hipEventRecord(e0);
+    kern_staged<MODE, WPS><<<blocks, 256>>>(out, dp, iters);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    best = ms < best ? ms : best;
+  }
+  const double mfmas = 42.0 * 56 * iters * blocks * 4, flops = mfmas * 16 * 16 * 32 * 2;
+  // per-wave time of one piece: a SIMD runs WPS * blocks_per_cu_x / 2 waves
+  printf("%-34s waves/SIMD=%d  %.3f ms  %.0f bf16 TF/s  %.1f%% of 2500  ns/piece/wave-slot %.1f\n", name,
+         WPS * blocks_per_cu_x / 2, best, flops / best / 1e9, flops / best / 1e9 / 25.0, best * 1e6 / (iters * 56));
+  (void)hipFree(out);
+  (void)hipFree(img);
+  (void)hipFree(dp);
+}
+
 int main() {
+  run_staged<6, 1>("staged sgemm_x3_piece", 2);
+  run_staged<6, 2>("staged sgemm_x3_piece", 2);
+  run_staged<7, 1>("staged pairs", 2);
+  run_staged<7, 2>("staged pairs", 2);
   run<0, 1>("sgemm_x3_piece (split)");
   run<0, 2>("sgemm_x3_piece (split)");
   run<1, 1>("sgemm_x3_piece (no split)");
