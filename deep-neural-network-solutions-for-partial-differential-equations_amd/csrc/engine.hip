@@ -94,8 +94,13 @@ struct dbsde_ctx {
   hipEvent_t ev_pipe[2] = {nullptr, nullptr};
   hipEvent_t ev_more[2] = {nullptr, nullptr};
   hipEvent_t ev_prof[2] = {nullptr, nullptr};
-  int chunks = 2;
+  // 0 = by size: two chunks only when one phase launch has more workgroups
+  // than the chip has slots (below that the chunks only serialize: A0, C0 || A1,
+  // C1 is three workgroup lifetimes against A, C's two); DBSDE_CHUNKS=n forces n
+  int chunks = 0;
   int chunk0 = 0;
+  int cus = 256;   // compute units of the device
+  int fv_slots = 0;   // resident phase workgroups of the chip (lazily queried)
   bool side_pending[2] = {false, false};
 
   // ---- network description
@@ -1539,6 +1544,9 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     if (e != hipSuccess || ndev == 0) rc = fail(c, DBSDE_EHIP, "no HIP device available");
     else if (cfg->device < 0 || cfg->device >= ndev) rc = fail(c, DBSDE_EINVAL, "bad device ordinal");
     else if ((e = hipSetDevice(cfg->device)) != hipSuccess) rc = fail(c, DBSDE_EHIP, hipGetErrorString(e));
+    else if ((e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, cfg->device)) != hipSuccess)
+      rc = fail(c, DBSDE_EHIP, hipGetErrorString(e));
+    if (const char* ec = getenv("DBSDE_CHUNKS")) c->chunks = std::max(0, atoi(ec));
   }
   if (!rc) rc = build_buffers(c);
   if (!rc) {
@@ -1863,7 +1871,15 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     // chunks of whole paths and whole WR-row tiles (WR paths = WR (N+1) rows =
     // N+1 tiles), WR = the variant's rows per workgroup
     const int WR = kFused[fv].rows;
-    int nch = grad ? c->chunks : 1;
+    // workgroup slots of the chip for this variant (two per CU for the
+    // 64-row kernels, one for the 512-register ones)
+    if (c->fv_slots == 0) {
+      int per = 0;
+      HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kFused[fv].A, 64 * P3_WAVES, 0));
+      c->fv_slots = std::max(1, per) * c->cus;
+    }
+    const int slots = c->fv_slots;
+    int nch = !grad ? 1 : (c->chunks > 0 ? c->chunks : (Rp / WR > slots ? 2 : 1));
     while (nch > 1 && (M % WR != 0 || (M / WR) % nch != 0)) --nch;
     if (nch <= 1) {
       RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));

@@ -211,6 +211,7 @@ __device__ __forceinline__ const float* lane_ptr(unsigned long long v, int idx) 
 //   NP > 0: the kernel's piece count at compile time (else the runtime n).
 template <int NBUF, int LC, int NF = 0, int NP = 0>
 struct PieceStagerT {
+  static constexpr int nbuf = NBUF;
   floatx4* wl;
   const float* const* img;
   const int* nf;
@@ -470,12 +471,28 @@ __device__ __forceinline__ void sgemm_x3_piece_pairs(Mat<TO>& acc, const Split3&
 #define DBSDE_A_RECOMP 0
 #endif
 
+// Vector-memory ops younger than piece KB's DMA (a lower bound for its
+// vm_wait), DIST = ring depth - 1 the DMA lead: the previous stage's epilogue
+// (NPRE ops, issued after the DMA of piece DIST - 1) for KB < DIST, and
+// `after` (NAFTER ops, issued at piece 0 after the DMA of piece DIST) for
+// 1 <= KB <= DIST.  A store is then waited for only once a DMA issued after
+// it is needed.  DBSDE_VMCOUNT 0: the earlier tighter counts (KB 0 NPRE, KB 1
+// NAFTER, none after), which made piece 1 wait for the epilogue's stores and
+// piece 2 for `after`'s.
+#ifndef DBSDE_VMCOUNT
+#define DBSDE_VMCOUNT 1
+#endif
+template <int KB, int DIST, int NPRE, int NAFTER>
+constexpr int piece_nyoung() {
+  if constexpr (DBSDE_VMCOUNT == 0) return KB == 0 ? NPRE : (KB == 1 ? NAFTER : 0);
+  return (KB < DIST ? NPRE : 0) + (KB >= 1 && KB <= DIST ? NAFTER : 0);
+}
 template <int TO, int TI, int NPRE, int NAFTER, int KB, bool PF, class SG, class F>
 __device__ __forceinline__ void stage_x3_from(Mat<TO>& acc, const Mat<TI>& b, SG& sg, int lane, F&& after,
                                               const Split3& s) {
   constexpr int NKB = (TI + 1) / 2;
   if constexpr (KB < NKB) {
-    const floatx4* w = sg.template next<KB == 0 ? NPRE : (KB == 1 ? NAFTER : 0)>();
+    const floatx4* w = sg.template next<piece_nyoung<KB, SG::nbuf - 1, NPRE, NAFTER>()>();
     if constexpr (KB == 0) {
       after();
       __builtin_amdgcn_sched_barrier(0);

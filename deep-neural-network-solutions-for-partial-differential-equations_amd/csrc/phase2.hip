@@ -65,7 +65,7 @@ __device__ __forceinline__ void stage_nt_from(Mat<TO> (&acc)[NT], const Mat<TI> 
                                               const Split3 (&s)[NT]) {
   constexpr int NKB = (TI + 1) / 2;
   if constexpr (KB < NKB) {
-    const floatx4* w = sg.template next<KB == 0 ? NPRE : (KB == 1 ? NAFTER : 0)>();
+    const floatx4* w = sg.template next<piece_nyoung<KB, SG::nbuf - 1, NPRE, NAFTER>()>();
     if constexpr (KB == 0) {
       after();
       __builtin_amdgcn_sched_barrier(0);

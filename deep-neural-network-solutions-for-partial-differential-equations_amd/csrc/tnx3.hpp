@@ -65,13 +65,23 @@ __device__ __forceinline__ void tx3_store(const TnX3Step& s, uintx4* img) {
 }
 
 // grid (tiles_m * tiles_n, splits, problems); rps = rows per split (multiple of 32)
+#ifndef DBSDE_TNX3_XCD
+#define DBSDE_TNX3_XCD 1
+#endif
+// XCD-aware order: workgroup i runs on XCD i % 8, so the grid is read as
+// eight contiguous runs of (tile, split, problem), one per XCD -- the tiles of
+// one split, which share their A / B column strips, run together on one XCD
+// and read the strips once into its L2 instead of once per tile.
 __global__ void __launch_bounds__(256) tn_x3_kernel(TNArgs args, int rps) {
-  const TNProb& P = args.prob[blockIdx.z];
+  const int nx = gridDim.x, ny = gridDim.y;
+  int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  const int per = nx * ny * gridDim.z / 8;
+  if (DBSDE_TNX3_XCD && lin < 8 * per) lin = (lin & 7) * per + (lin >> 3);
+  const int tile = lin % nx, split = (lin / nx) % ny, prob = lin / (nx * ny);
+  const TNProb& P = args.prob[prob];
   const int tiles_n = (P.nB[0] + TX_TILE - 1) / TX_TILE, tiles_m = (P.nA[0] + TX_TILE - 1) / TX_TILE;
-  const int tile = blockIdx.x;
   if (tile >= tiles_m * tiles_n) return;
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-  const int split = blockIdx.y;
   const int r_begin = split * rps, r_end = min(r_begin + rps, args.Rp);
   const int nstep = r_end > r_begin ? (r_end - r_begin) / 32 : 0;
   __shared__ uintx4 sa[8 * 3 * 64], sb[8 * 3 * 64];

@@ -1,6 +1,6 @@
 #!/bin/bash
 mkdir -p gpurun_out/ub
-timeout -k 10 200 tools/ubench/piece_x3 > gpurun_out/ub/piece3.txt 2>&1
+timeout -k 10 200 tools/ubench/piece_x3 > gpurun_out/ub/piece5.txt 2>&1
 rc=$?
-cat gpurun_out/ub/piece3.txt
+cat gpurun_out/ub/piece5.txt
 exit $rc

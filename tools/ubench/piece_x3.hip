@@ -150,8 +150,13 @@ __device__ __forceinline__ void one_piece(Mat<7>& acc, const Split3& s, const fl
 // ring, LDS-DMA of each piece two ahead from a 56-piece image in global memory
 // (L2 resident), counted vmcnt wait + barrier per piece) around
 // sgemm_x3_piece (6) or the pairs piece (7)
+// mode 8: mode 6 plus the phase kernels' activation stores: after every 4th
+// piece (one level) the wave stores its 16 x 112 accumulator tile twice (as
+// fstore + bstore_stream do: 2 x 7 KiB per level and wave) into a large
+// streaming buffer -- the HBM write stream of phase A (~185 MB per dispatch)
 template <int MODE, int WPS>
-__global__ void __launch_bounds__(256, WPS) kern_staged(float* out, const float* const* pieces, int iters) {
+__global__ void __launch_bounds__(256, WPS) kern_staged(float* out, const float* const* pieces, int iters,
+                                                       float* sink, long long sink_floats) {
   constexpr int BUF = 3 * 7 * 64;
   __shared__ floatx4 wl[P3_NBUF_X3 * BUF];
   const int lane = threadIdx.x & 63;
@@ -163,13 +168,35 @@ __global__ void __launch_bounds__(256, WPS) kern_staged(float* out, const float*
     acc.v[t] = floatx4{0.f, 0.f, 0.f, 0.f};
   }
   Split3 s = split_block<7, 0>(b);
+  long long so = ((long long)blockIdx.x * 4 + wave) * 16 * 112 * 14;
   for (int it = 0; it < iters; ++it) {
     PieceStagerT<P3_NBUF_X3, 5, 21, 56> sg{wl, pieces, nullptr, 56, 0, wave, lane, BUF};
     sg.start();
     SFor<0, 56>::run([&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
       const floatx4* w = sg.template next<0>();
+      if constexpr (MODE == 8 && k % 4 == 0 && k > 0) {
+        float* base = sink + (so % (sink_floats - 2 * 16 * 112)) ;
+        fstore(acc, base, 112, 0, 0);
+        bstore_stream(acc, base + 16 * 112, 112, 0, 0);
+        so += (long long)gridDim.x * 4 * 16 * 112 * 2;
+      }
+      if constexpr (MODE == 9 && k >= 4) {   // the same bytes, 3 or 4 of the 14 stores after each piece's barrier
+        float* base = sink + (so % (sink_floats - 2 * 16 * 112));
+        constexpr int i0 = (k % 4) * 4, i1 = i0 + 4 < 14 ? i0 + 4 : 14;
+        const int l = threadIdx.x & 63;
+#pragma unroll
+        for (int i = i0; i < i1; ++i) {
+          if (i < 7)
+            *(floatx4*)(base + 256 * i + 4 * l) = acc.v[i < 7 ? i : 0];
+          else
+            __builtin_nontemporal_store(acc.v[i - 7 < 7 ? i - 7 : 0],
+                                        (floatx4*)(base + 16 * 112 + (l & 15) * 112 + 4 * (l >> 4) + 16 * (i - 7)));
+        }
+        if (k % 4 == 3) so += (long long)gridDim.x * 4 * 16 * 112 * 2;
+      }
       uintx4 sn[3];
-      if constexpr (MODE == 6)
+      if constexpr (MODE == 6 || MODE == 8 || MODE == 9)
         sgemm_x3_piece<7, 7, 1, true>(acc, s, w, lane, b, sn);
       else
         sgemm_x3_piece_pairs<7, 7, 1>(acc, s, w, lane, b, sn);
@@ -255,11 +282,14 @@ void run_staged(const char* name, int blocks_per_cu_x) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  kern_staged<MODE, WPS><<<blocks, 256>>>(out, dp, iters);
+  const long long sink_floats = 256LL << 20;   // 1 GiB streaming target
+  float* sink;
+  (void)hipMalloc(&sink, sink_floats * 4);
+  kern_staged<MODE, WPS><<<blocks, 256>>>(out, dp, iters, sink, sink_floats);
   float best = 1e30f;
   for (int r = 0; r < 3; ++r) {
     (void)hipEventRecord(e0);
-    kern_staged<MODE, WPS><<<blocks, 256>>>(out, dp, iters);
+    kern_staged<MODE, WPS><<<blocks, 256>>>(out, dp, iters, sink, sink_floats);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
@@ -273,13 +303,17 @@ void run_staged(const char* name, int blocks_per_cu_x) {
   (void)hipFree(out);
   (void)hipFree(img);
   (void)hipFree(dp);
+  (void)hipFree(sink);
 }
 
 int main() {
   run_staged<6, 1>("staged sgemm_x3_piece", 2);
   run_staged<6, 2>("staged sgemm_x3_piece", 2);
-  run_staged<7, 1>("staged pairs", 2);
-  run_staged<7, 2>("staged pairs", 2);
+  run_staged<8, 1>("staged + level stores", 2);
+  run_staged<8, 2>("staged + level stores", 2);
+  run_staged<9, 1>("staged + spread stores", 2);
+  run_staged<9, 2>("staged + spread stores", 2);
+  return 0;
   run<0, 1>("sgemm_x3_piece (split)");
   run<0, 2>("sgemm_x3_piece (split)");
   run<1, 1>("sgemm_x3_piece (no split)");
