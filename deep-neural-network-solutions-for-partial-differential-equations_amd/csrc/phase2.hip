@@ -7,6 +7,11 @@
 #define DBSDE_DEVICE_HELPERS_ONLY
 #include "phase2.hpp"
 
+// fragment pairs in the one-tile kernels: bit 0 phase A, bit 1 phase C
+#ifndef DBSDE_P2_PAIRS
+#define DBSDE_P2_PAIRS 3
+#endif
+
 namespace dbsde {
 
 // stager: split-bf16 pieces; T == TD: every piece 3 T fragments (compile-time
@@ -60,7 +65,7 @@ __device__ __forceinline__ void sgemm_x3_piece_nt(Mat<TO> (&acc)[NT], const Spli
   });
 }
 
-template <int TO, int TI, int NPRE, int NAFTER, int KB, int NT, class SG, class F>
+template <int TO, int TI, int NPRE, int NAFTER, int KB, int NT, bool PR, class SG, class F>
 __device__ __forceinline__ void stage_nt_from(Mat<TO> (&acc)[NT], const Mat<TI> (&b)[NT], SG& sg, int lane, F&& after,
                                               const Split3 (&s)[NT]) {
   constexpr int NKB = (TI + 1) / 2;
@@ -71,25 +76,31 @@ __device__ __forceinline__ void stage_nt_from(Mat<TO> (&acc)[NT], const Mat<TI> 
       __builtin_amdgcn_sched_barrier(0);
     }
     uintx4 sn[NT][3];
-    sgemm_x3_piece_nt<TO, TI, KB + 1, NT>(acc, s, w, lane, b, sn);
+    if constexpr (PR && NT == 1)
+      sgemm_x3_piece_pairs<TO, TI, KB + 1>(acc[0], s[0], w, lane, b[0], sn[0]);
+    else
+      sgemm_x3_piece_nt<TO, TI, KB + 1, NT>(acc, s, w, lane, b, sn);
     if constexpr (KB + 1 < NKB) {
       Split3 s2[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         s2[t] = Split3{__builtin_bit_cast(bf16x8, sn[t][0]), __builtin_bit_cast(bf16x8, sn[t][1]),
                        __builtin_bit_cast(bf16x8, sn[t][2])};
-      stage_nt_from<TO, TI, NPRE, NAFTER, KB + 1, NT>(acc, b, sg, lane, after, s2);
+      stage_nt_from<TO, TI, NPRE, NAFTER, KB + 1, NT, PR>(acc, b, sg, lane, after, s2);
     }
   }
 }
 // one stage = one operand image, one piece per 32-wide input block; `after`
 // runs right after the first piece's barrier.  NPRE / NAFTER as stage_mm.
-template <int TO, int TI, int NPRE, int NAFTER, int NT, class SG, class F>
+//   PR: one tile per wave (one wave per SIMD) -- the fragments in pairs, two
+//   interleaved MFMA chains (sgemm_x3_piece_pairs): a lone wave cannot hide
+//   the dependent issue of one chain (tools/ubench/piece_x3.hip: 59 -> 76 %)
+template <int TO, int TI, int NPRE, int NAFTER, int NT, bool PR = false, class SG, class F>
 __device__ __forceinline__ void stage_nt(Mat<TO> (&acc)[NT], const Mat<TI> (&b)[NT], SG& sg, int lane, F&& after) {
   Split3 s[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) s[t] = split_block<TI, 0>(b[t]);
-  stage_nt_from<TO, TI, NPRE, NAFTER, 0, NT>(acc, b, sg, lane, after, s);
+  stage_nt_from<TO, TI, NPRE, NAFTER, 0, NT, PR>(acc, b, sg, lane, after, s);
 }
 
 template <int NT, int TT>
@@ -105,6 +116,7 @@ __device__ __forceinline__ void zero_nt(Mat<TT> (&m)[NT]) {
 template <int T, int TD, int K, int ACT, bool HV, int NT, int NBUF, bool ADOT>
 __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p) {
   constexpr int TB = T > TD ? T : TD, BUF = 3 * TB * 64, ROWS = 16 * NT * P3_WAVES;
+  constexpr bool PRA = NT == 1 && (DBSDE_P2_PAIRS & 1);
   __shared__ floatx4 wl[NBUF * BUF];
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -119,7 +131,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p) 
 
   Mat<T> h[NT], acc[NT];
   zero_nt(acc);
-  stage_nt<T, TD, NT * TD, 0, NT>(acc, x, sg, lane, NoOp{});
+  stage_nt<T, TD, NT * TD, 0, NT, PRA>(acc, x, sg, lane, NoOp{});
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     fstore(acc[t], p.Abuf, S, row0 + 16 * t, 0);
@@ -135,11 +147,11 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p) 
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero_nt(acc);
-    stage_nt<T, T, NT * T, NT * T, NT>(acc, h, sg, lane, [&]() __attribute__((always_inline)) {
+    stage_nt<T, T, NT * T, NT * T, NT, PRA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) bstore_stream(h[t], p.H, S, row0 + 16 * t, (j - 1) * Wd);
     });
-    if constexpr (HV) stage_nt<T, TD, 0, 0, NT>(acc, x, sg, lane, NoOp{});
+    if constexpr (HV) stage_nt<T, TD, 0, 0, NT, PRA>(acc, x, sg, lane, NoOp{});
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       if constexpr (!HV) {
@@ -214,10 +226,10 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p) 
     zero_nt(gn);
     constexpr int NPREV = NT * ((j < K ? 2 * T : T) + T);
     if constexpr (HV) {
-      stage_nt<TD, T, 0, NPREV, NT>(z, dl, sg, lane, prev);   // Z += delta_j V_j
-      stage_nt<T, T, 0, 0, NT>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
+      stage_nt<TD, T, 0, NPREV, NT, PRA>(z, dl, sg, lane, prev);   // Z += delta_j V_j
+      stage_nt<T, T, 0, 0, NT, PRA>(gn, dl, sg, lane, NoOp{});     // delta_j B_j
     } else {
-      stage_nt<T, T, 0, NPREV, NT>(gn, dl, sg, lane, prev);
+      stage_nt<T, T, 0, NPREV, NT, PRA>(gn, dl, sg, lane, prev);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -230,7 +242,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p) 
           dl[t].v[o][r] = gv * act_1<ACT>(av[t].v[o][r]);
         }
   });
-  stage_nt<TD, T, 0, NT * (2 * T + TD), NT>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
+  stage_nt<TD, T, 0, NT * (2 * T + TD), NT, PRA>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       fstore(g[t], p.G, S, row0 + 16 * t, 0);
@@ -294,6 +306,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseA2_kernel(FusedArgs p) 
 template <int T, int TD, int K, int ACT, bool HV, int NT, int NBUF, bool ADOT>
 __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) {
   constexpr int TB = T > TD ? T : TD, BUF = 3 * TB * 64, ROWS = 16 * NT * P3_WAVES;
+  constexpr bool PRC = NT == 1 && (DBSDE_P2_PAIRS & 2) && ACT != ACT_TANH;   // tanh: spills with pairs
   // one __shared__ array (the loss slots after the ring): see phaseC_kernel
   __shared__ floatx4 wl[NBUF * BUF + P3_WAVES / 2];
   double* lsum = (double*)(wl + NBUF * BUF);
@@ -360,7 +373,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
   Mat<T> hd[NT], av[NT];
   constexpr bool XFIRST = HV && !ADOT;
   zero_nt(ad[0]);
-  stage_nt<T, TD, NT * TD, NT * T, NT>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
+  stage_nt<T, TD, NT * TD, NT * T, NT, PRC>(ad[0], zb, sg, lane, [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) fload(av[t], p.Abuf, S, row0 + 16 * t, 0);
     if (threadIdx.x == 0) {   // fixed-order pairwise tree over the waves
@@ -378,7 +391,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
     SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
       constexpr int j = decltype(jc)::value;
       zero_nt(ad[j]);
-      stage_nt<T, TD, 0, 0, NT>(ad[j], zb, sg, lane, NoOp{});
+      stage_nt<T, TD, 0, 0, NT, PRC>(ad[j], zb, sg, lane, NoOp{});
     });
   }
 #pragma unroll
@@ -397,13 +410,13 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
     }
     if constexpr (!XFIRST) zero_nt(ad[ja]);
     constexpr int NAF = 2 * NT * T;   // (ADOT: the Adot stores are older, not counted)
-    stage_nt<T, T, 0, NAF, NT>(ad[ja], hd, sg, lane, [&]() __attribute__((always_inline)) {
+    stage_nt<T, T, 0, NAF, NT, PRC>(ad[ja], hd, sg, lane, [&]() __attribute__((always_inline)) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) bstore_stream(hd[t], p.Hdot, S, row0 + 16 * t, (j - 1) * Wd);
 #pragma unroll
       for (int t = 0; t < NT; ++t) fload(av[t], p.Abuf, S, row0 + 16 * t, j * Wd);
     });
-    if constexpr (HV && !XFIRST) stage_nt<T, TD, 0, 0, NT>(ad[ja], zb, sg, lane, NoOp{});
+    if constexpr (HV && !XFIRST) stage_nt<T, TD, 0, 0, NT, PRC>(ad[ja], zb, sg, lane, NoOp{});
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -443,7 +456,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p) 
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) pv[t].v[o][rr] *= p.rho;
     constexpr int NAF = (ADOT ? 4 : 3) * NT * T;
-    stage_nt<T, T, 0, NAF, NT>(pv, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
+    stage_nt<T, T, 0, NAF, NT, PRC>(pv, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
 #pragma unroll
       for (int t = 0; t < NT; ++t) bstore_stream(al[t], p.Alpha, S, row0 + 16 * t, j * Wd);
 #pragma unroll

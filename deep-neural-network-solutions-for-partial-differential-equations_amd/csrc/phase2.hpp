@@ -40,13 +40,15 @@ template <int T, int TD, int K, int ACT, bool HV, int NT, int NBUF, bool ADOT>
 __global__ void __launch_bounds__(64 * P3_WAVES, 1) phaseC2_kernel(FusedArgs p);
 
 // the instantiations phase2.hip builds (its own translation unit, compiled in
-// parallel with engine.hip): config 4's FC [101,256x4,1], one tile per wave,
-// 48 KiB pieces, adot through memory.  (The width-112 networks with two tiles
+// parallel with engine.hip): config 4's FC [101,256x4,1] and config 1's FC
+// [2,256x4,1] (call_option_1d.py), one tile per wave, 48 KiB pieces, adot
+// through memory.  (The width-112 networks with two tiles
 // per wave, X(7, 7, 3, ACT, HV, 2, 4, ADOT), measured slower than phase.hpp's
 // two 4-wave workgroups per CU: 0.386 / 0.406 ms against 0.293 ms for the
 // phase section at the north star)
-#define DBSDE_PHASE2_INSTANCES(X) \
-  X(16, 7, 3, 0, false, 1, 3, true) X(16, 7, 3, 1, false, 1, 3, true) X(16, 7, 3, 2, false, 1, 3, true)
+#define DBSDE_PHASE2_INSTANCES(X)                                                                   \
+  X(16, 7, 3, 0, false, 1, 3, true) X(16, 7, 3, 1, false, 1, 3, true) X(16, 7, 3, 2, false, 1, 3, true) \
+  X(16, 1, 3, 0, false, 1, 3, true) X(16, 1, 3, 1, false, 1, 3, true) X(16, 1, 3, 2, false, 1, 3, true)
 #define DBSDE_PHASE2_EXTERN(T, TD, K, ACT, HV, NT, NBUF, ADOT)                                   \
   extern template __global__ void phaseA2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>(FusedArgs); \
   extern template __global__ void phaseC2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>(FusedArgs);

@@ -18,6 +18,10 @@
 // MFMAs of the previous block (x3_products).
 #include "tnw.hpp"
 
+#ifndef DBSDE_TNW_INTERLEAVE
+#define DBSDE_TNW_INTERLEAVE 1
+#endif
+
 namespace dbsde {
 
 namespace {
@@ -115,6 +119,23 @@ __device__ __forceinline__ void x3_products(floatx4 (&acc)[NB][NB], const TNWPro
 #pragma unroll
         for (int j = 0; j < 8; ++j) ra[m + 1][j] = bload1(rA, voa + 64u * (m + 1), (unsigned)j * lda);
       }
+#if DBSDE_TNW_INTERLEAVE
+      // product-major: the NB accumulators of the row advance one product at
+      // a time, so consecutive MFMAs are independent (a lone wave per SIMD
+      // cannot hide the issue latency of a dependent chain of six)
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.l, sb[n].h, acc[m][n]);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.h, sb[n].l, acc[m][n]);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.m, sb[n].m, acc[m][n]);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.m, sb[n].h, acc[m][n]);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.h, sb[n].m, acc[m][n]);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.h, sb[n].h, acc[m][n]);
+#else
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
         floatx4 c = acc[m][n];
@@ -125,6 +146,7 @@ __device__ __forceinline__ void x3_products(floatx4 (&acc)[NB][NB], const TNWPro
         c = mfma_bf(sa.h, sb[n].m, c);
         acc[m][n] = mfma_bf(sa.h, sb[n].h, c);
       }
+#endif
 #pragma unroll
       for (int k = 0; k < 6 * NB; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA

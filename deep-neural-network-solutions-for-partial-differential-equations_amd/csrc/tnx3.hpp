@@ -128,18 +128,15 @@ __global__ void __launch_bounds__(256) tn_x3_kernel(TNArgs args, int rps) {
       for (int p = 0; p < 3; ++p) fa[p] = sa[((4 * wm + m) * 3 + p) * 64 + lane];
       const bf16x8 ah = __builtin_bit_cast(bf16x8, fa[0]), am = __builtin_bit_cast(bf16x8, fa[1]),
                    al = __builtin_bit_cast(bf16x8, fa[2]);
+      // product-major over the four accumulators of the row: consecutive
+      // MFMAs are independent (no dependent chain of six)
+      const bf16x8 a6[6] = {al, ah, am, am, ah, ah};
+      constexpr int bp[6] = {0, 2, 1, 0, 1, 0};   // b part: 0 hi, 1 mid, 2 lo
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const bf16x8 bh = __builtin_bit_cast(bf16x8, fb[n][0]), bm = __builtin_bit_cast(bf16x8, fb[n][1]),
-                     bl = __builtin_bit_cast(bf16x8, fb[n][2]);
-        floatx4 c = acc[m][n];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, c, 0, 0, 0);
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
-      }
+      for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a6[k], __builtin_bit_cast(bf16x8, fb[n][bp[k]]), acc[m][n], 0, 0, 0);
     }
     __syncthreads();
   }

@@ -188,12 +188,14 @@ def test_fused_update_with_a_prefetched_rollout_beside_it(pkg, dev):
         torch.testing.assert_close(x, y, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("name", ["g1_w256_hjb_FC_Sine_N20.npz"])
+@pytest.mark.parametrize("name", ["g1_w256_hjb_FC_Sine_N20.npz", "g1_w256_oned_call_FC_Sine_M16_N5.npz",
+                                  "g1_w256_oned_call_FC_Sine_M256_N50.npz"])
 def test_width256_fused_kernels_match_reference(pkg, dev, name):
-    """Config 4's FC-Sine [101,256x4,1] (hjb_implement.py:590-604) on the
-    fused width-256 phase kernels (phase2.hip, one 16-row tile per wave, adot
-    through memory; the default, DBSDE_W256=1 made explicit) against the
-    reference fixture, tolerances as test_gpu_parity."""
+    """Config 4's FC-Sine [101,256x4,1] (hjb_implement.py:590-604) and config
+    1's FC-Sine [2,256x4,1] (call_option_1d.py) on the fused width-256 phase
+    kernels (phase2.hip, one 16-row tile per wave, adot through memory; the
+    default, DBSDE_W256=1 made explicit) against the reference fixtures,
+    tolerances as test_gpu_parity."""
     from test_gpu_parity import make_solver
     g = _load(name)
     old = os.environ.get("DBSDE_W256")
@@ -226,3 +228,36 @@ def test_width256_fused_kernels_match_reference(pkg, dev, name):
     used = g["used"]
     r = grad.cpu().numpy()
     np.testing.assert_allclose(r[used], g["grad"][used], rtol=0, atol=2e-4 * np.abs(g["grad"]).max())
+
+
+@pytest.mark.parametrize("M", [128, 1024])
+def test_phase_chunk_count_does_not_change_the_step(pkg, dev, M):
+    """The phase pipeline's path chunks (DBSDE_CHUNKS; default by occupancy:
+    one chunk when a phase launch fits the chip's workgroup slots, M = 128,
+    else two, M = 1024) only reorder independent rows: loss and gradient are
+    bit-identical for 1, 2 and the default."""
+    g = _load("g2_north_star.npz")
+    layers = [int(v) for v in g["layers"]]
+    D = layers[0] - 1
+    res = {}
+    old = os.environ.get("DBSDE_CHUNKS")
+    try:
+        for ch in ("1", "2", None):
+            if ch is None:
+                os.environ.pop("DBSDE_CHUNKS", None)
+            else:
+                os.environ["DBSDE_CHUNKS"] = ch
+            m = pkg.BlackScholesBarenblatt(g["Xi"], 1.0, M, 50, D, layers, "NAIS-Net", "Sine", device=dev)
+            m.params.copy_(torch.from_numpy(g["params"]).to(dev))
+            loss = torch.empty(1, device=dev)
+            m.solver.loss_grad(m.params, M, 50, m._device_xi(0, M), seed=5, grad=m.grad, loss=loss)
+            torch.cuda.synchronize()
+            res[ch] = (loss.cpu().clone(), m.grad.cpu().clone())
+    finally:
+        if old is None:
+            os.environ.pop("DBSDE_CHUNKS", None)
+        else:
+            os.environ["DBSDE_CHUNKS"] = old
+    for ch in ("2", None):
+        torch.testing.assert_close(res[ch][0], res["1"][0], rtol=0, atol=0)
+        torch.testing.assert_close(res[ch][1], res["1"][1], rtol=0, atol=0)
