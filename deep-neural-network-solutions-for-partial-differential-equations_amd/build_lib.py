@@ -12,7 +12,7 @@ CSRC = os.path.join(HERE, "csrc")
 # translation units and their extra flags: the weight-gradient kernel is built
 # with VGPR-form MFMA (see csrc/tnw.hip); everything else (its split-bf16 form
 # tnwx3.hip included: accumulators in AGPRs) with the defaults
-UNITS = [("engine.hip", []), ("phase2.hip", []), ("evals.hip", []), ("tnw.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]),
+UNITS = [("engine.hip", []), ("phase2.hip", []), ("phasecs.hip", []), ("evals.hip", []), ("tnw.hip", ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]),
          ("tnwx3.hip", [])]
 DEPS = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC)) if f.endswith((".hip", ".hpp"))] + \
     [os.path.join(ROOT, "include", "dbsde.h")]

@@ -26,6 +26,7 @@
 #include "paths.hpp"
 #include "phase.hpp"
 #include "phase2.hpp"
+#include "phasecs.hpp"
 #include "chainx3.hpp"
 #include "tnx3.hpp"
 #include "tnw.hpp"
@@ -100,7 +101,9 @@ struct dbsde_ctx {
   int chunks = 0;
   int chunk0 = 0;
   int cus = 256;   // compute units of the device
-  int fv_slots = 0;   // resident phase workgroups of the chip (lazily queried)
+  int fv_slots[64] = {0};   // resident workgroups of the chip per phase variant (lazily queried)
+  int fv_cs = -1;           // the column-split variant of fv (phasecs.hpp), or -1
+  int cs_mode = 2;          // 0 off, 1 always, 2 by batch size
   bool side_pending[2] = {false, false};
 
   // ---- network description
@@ -307,27 +310,35 @@ struct FusedVariant {
 #define FQ(T, TD, K, ACT, HV, NT, NBUF, ADOT)                                                              \
   {T, TD, K, ACT, HV, 1, 64 * NT, ADOT, (HV) && !(ADOT), phaseA2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>, \
    phaseC2_kernel<T, TD, K, ACT, HV, NT, NBUF, ADOT>},
+// column-split kernels (phasecs.hpp): 16 rows per workgroup, the small-M form
+#define FCS(T, TD, K, ACT, HV) \
+  {T, TD, K, ACT, HV, 1, CS_ROWS, 0, (HV), phaseAcs_kernel<T, TD, K, ACT, HV>, phaseCcs_kernel<T, TD, K, ACT, HV>},
 const FusedVariant kFused[] = {
     DBSDE_PHASE2_INSTANCES(FQ)
+    DBSDE_PHASECS_INSTANCES(FCS)
     FV2(7, 7, 3, 0, 1), FV2(7, 7, 3, 1, 1), FV2(7, 7, 3, 2, 1), FV2(7, 7, 3, 0, 0), FV2(7, 7, 3, 1, 0),
     FV2(7, 7, 3, 2, 0), FV2(1, 1, 1, 0, 0), FV2(1, 1, 1, 1, 0), FV2(1, 1, 1, 2, 0), FV2(1, 1, 2, 0, 0),
     FV2(1, 1, 2, 1, 0), FV2(1, 1, 2, 2, 0), FV2(1, 1, 3, 0, 0), FV2(1, 1, 3, 1, 0), FV2(1, 1, 3, 2, 0),
 };
 #undef FQ
+#undef FCS
 #undef FV2
 #undef FV
 constexpr int kNumFused = (int)(sizeof(kFused) / sizeof(kFused[0]));
+static_assert(kNumFused <= 64, "dbsde_ctx::fv_slots");
 // the variant for a network: rows_max 128 admits the two-tile kernels
 // (preferred when admitted), 64 only the others; adot selects between the
 // register and the memory adot form where both exist
 // (DBSDE_W256=0 leaves the width-256 FC networks to the per-layer chain)
-int fused_variant(int T, int TD, int K, int act, bool hv, bool x3, int rows_max = P3_ROWS, bool adot = false) {
+// (cs: the column-split variant, which the launch picks for small batches)
+int fused_variant(int T, int TD, int K, int act, bool hv, bool x3, int rows_max = P3_ROWS, bool adot = false,
+                  bool cs = false) {
   const char* ew = getenv("DBSDE_W256");
   const bool wide = !(ew && ew[0] == '0');
   int any = -1;
   for (int i = 0; i < kNumFused; ++i)
     if ((wide || kFused[i].T <= 8) && kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv &&
-        kFused[i].x3 == (int)x3 && kFused[i].rows <= rows_max) {
+        kFused[i].x3 == (int)x3 && kFused[i].rows <= rows_max && (kFused[i].rows == CS_ROWS) == cs) {
       if (kFused[i].adot == (int)adot) return i;
       if (any < 0) any = i;
     }
@@ -441,6 +452,15 @@ int build_net(dbsde_ctx* c) {
   c->fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3, c->nt2 ? Q_ROWS : P3_ROWS,
                                    c->adot)
                    : -1;
+  // the column-split form for small batches (DBSDE_CS=0 never, =1 always,
+  // default when the 64-row kernels would fill at most half the chip's slots)
+  {
+    const char* ecs = getenv("DBSDE_CS");
+    c->cs_mode = !ecs ? 2 : (ecs[0] == '0' ? 0 : 1);
+    c->fv_cs = (c->fv >= 0 && c->cs_mode && kFused[c->fv].rows == P3_ROWS && c->x3)
+                   ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, true, P3_ROWS, false, true)
+                   : -1;
+  }
   // FC / Resnet layouts the fused kernels do not cover: split-bf16 chain GEMMs
   // (uniform hidden width, output blocks a multiple of the column tile)
   // (the same layouts' weight-gradient tiles run split-bf16 behind the fused
@@ -1547,6 +1567,7 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     else if ((e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, cfg->device)) != hipSuccess)
       rc = fail(c, DBSDE_EHIP, hipGetErrorString(e));
     if (const char* ec = getenv("DBSDE_CHUNKS")) c->chunks = std::max(0, atoi(ec));
+    if (const char* ec = getenv("DBSDE_CHUNK0")) c->chunk0 = std::max(0, atoi(ec));
   }
   if (!rc) rc = build_buffers(c);
   if (!rc) {
@@ -1859,7 +1880,10 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   int nloss_parts;
   bool tnw_piped = false;
   FusedArgs fa;
-  const int fv = c->fv;
+  int fv = c->fv;
+  // small batches: the column-split kernels when the 64-row ones would fill
+  // at most half of their workgroup slots (M <= 256 at the north star)
+  if (fv >= 0 && c->fv_cs >= 0 && (c->cs_mode == 1 || Rp / P3_ROWS <= c->cus)) fv = c->fv_cs;
   if (fv >= 0) {
     fa = fused_args(c, R, Rp, N1, q3);
     if (!fused_piece_counts_ok(c, fa)) return fail(c, DBSDE_EINVAL, "internal: fused kernel piece counts");
@@ -1873,12 +1897,12 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     const int WR = kFused[fv].rows;
     // workgroup slots of the chip for this variant (two per CU for the
     // 64-row kernels, one for the 512-register ones)
-    if (c->fv_slots == 0) {
+    if (c->fv_slots[fv] == 0) {
       int per = 0;
       HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kFused[fv].A, 64 * P3_WAVES, 0));
-      c->fv_slots = std::max(1, per) * c->cus;
+      c->fv_slots[fv] = std::max(1, per) * c->cus;
     }
-    const int slots = c->fv_slots;
+    const int slots = c->fv_slots[fv];
     int nch = !grad ? 1 : (c->chunks > 0 ? c->chunks : (Rp / WR > slots ? 2 : 1));
     while (nch > 1 && (M % WR != 0 || (M / WR) % nch != 0)) --nch;
     if (nch <= 1) {

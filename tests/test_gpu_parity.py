@@ -57,18 +57,23 @@ def dev():
     return torch.device("cuda:0")
 
 
-def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=1):
+def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=1, cs=None):
     """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at
     create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0); x3=False
     the fp32-input MFMA form of the fused phase and weight-gradient kernels
     (DBSDE_X3=0 / DBSDE_TNW_X3=0) instead of the split-bf16 one; nt=1 the
     one-tile-per-wave phase kernels (DBSDE_NT=1) where the two-tile ones
-    (phase2.hip) exist."""
+    (phase2.hip) exist; cs "0" / "1" never / always the column-split phase
+    kernels (phasecs.hip; default: by batch size, so the small fixtures run
+    them)."""
     layers = [int(v) for v in g["layers"]]
     D = layers[0] - 1
     env = {"DBSDE_FUSED": "1" if fused else "0", "DBSDE_TNW": "1" if tnw else "0",
            "DBSDE_X3": "1" if x3 else "0", "DBSDE_TNW_X3": "1" if x3 else "0", "DBSDE_NT": str(nt)}
-    old = {k: os.environ.get(k) for k in env}
+    old = {k: os.environ.get(k) for k in list(env) + ["DBSDE_CS"]}
+    os.environ.pop("DBSDE_CS", None)
+    if cs is not None:
+        env["DBSDE_CS"] = cs
     os.environ.update(env)
     try:
         return pkg.NativeSolver(str(g["mode"]), layers, str(g["activation"]),
@@ -81,10 +86,10 @@ def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=1):
                 os.environ[k] = v
 
 
-def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, nt=1):
+def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, nt=1, cs=None):
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
-    s = make_solver(pkg, dev, g, fused, x3=x3, nt=nt)
+    s = make_solver(pkg, dev, g, fused, x3=x3, nt=nt, cs=cs)
     params = torch.from_numpy(g["params"]).to(dev)
     out = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (N + 1) * D, device=dev),
                Y=torch.empty(M * (N + 1), device=dev), Z=torch.empty(M * (N + 1) * D, device=dev))
@@ -103,14 +108,17 @@ def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, nt=1):
     return res
 
 
-@pytest.mark.parametrize("fused", ["fused", "fused_fp32", "chain"])
+@pytest.mark.parametrize("fused", ["fused", "fused_64row", "fused_fp32", "chain"])
 @pytest.mark.parametrize("path", G1, ids=[os.path.basename(p)[3:-4] for p in G1])
 def test_loss_grad_matches_reference(pkg, dev, path, fused):
     """fused: the default fused kernels (split-bf16 matrix form at width
-    110/112 and, for FC, 256); fused_fp32: the fused kernels on fp32-input
-    MFMA; chain: the per-layer GEMM path."""
+    110/112 and, for FC, 256; at these small batches the column-split form
+    where it exists); fused_64row: the same with the 64-row kernels
+    (DBSDE_CS=0); fused_fp32: the fused kernels on fp32-input MFMA; chain: the
+    per-layer GEMM path."""
     g = _load(path)
-    r = native_case(pkg, dev, g, fused=fused != "chain", x3=fused == "fused")
+    r = native_case(pkg, dev, g, fused=fused != "chain", x3=fused in ("fused", "fused_64row"),
+                    cs="0" if fused == "fused_64row" else None)
     if str(g["problem"]) == "heston":
         # the reference's torch.sqrt on the CPU is MKL vsSqrt (ATen vml), which
         # is not correctly rounded at near-ties; the kernel's sqrt is (as numpy's,
@@ -271,12 +279,13 @@ def test_net_u_matches_fixture_Y(pkg, dev):
     np.testing.assert_allclose(du.cpu().numpy(), g["Z"].reshape(R, D), rtol=0, atol=1e-4)
 
 
-@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False), dict(x3=False)],
-                         ids=["chain", "splitk_weight_grad", "fp32_mfma"])
+@pytest.mark.parametrize("variant", [dict(fused=False), dict(tnw=False), dict(x3=False), dict(cs="1")],
+                         ids=["chain", "splitk_weight_grad", "fp32_mfma", "column_split"])
 def test_kernel_paths_agree_at_north_star(pkg, dev, variant):
     """The default kernels (fused phases + wave-owned weight-gradient tiles)
-    against the per-layer chain path and against the split-K weight-gradient
-    GEMM, on the full north-star batch (same params and W)."""
+    against the per-layer chain path, the split-K weight-gradient GEMM, the
+    fp32-input MFMA form and the column-split phase kernels (forced at
+    M = 1024), on the full north-star batch (same params and W)."""
     g = _load(os.path.join(GOLDEN, "g2_north_star.npz"))
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])

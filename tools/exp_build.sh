@@ -12,7 +12,7 @@ while [ $# -ge 2 ]; do
   mkdir -p $PKG/lib/exp/$name
   ( $H $F $defs -c -o $PKG/lib/exp/$name/engine.o $PKG/csrc/engine.hip && \
     $H --offload-arch=gfx950 -shared -fPIC -o $PKG/lib/exp/$name/libdbsde.so $PKG/lib/exp/$name/engine.o \
-       $PKG/lib/obj/phase2.o $PKG/lib/obj/evals.o $PKG/lib/obj/tnw.o $PKG/lib/obj/tnwx3.o && \
+       $PKG/lib/obj/phase2.o $PKG/lib/obj/phasecs.o $PKG/lib/obj/evals.o $PKG/lib/obj/tnw.o $PKG/lib/obj/tnwx3.o && \
     rm $PKG/lib/exp/$name/engine.o && echo "built $name" ) &
   pids+=($!)
 done
