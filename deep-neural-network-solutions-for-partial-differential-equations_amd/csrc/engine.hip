@@ -178,6 +178,7 @@ struct dbsde_ctx {
   // wave-owned weight-gradient tiles (tnw.hpp): NAIS layouts with Dp == Wp
   bool tnw = false;
   int tnw_nb = 0, tnw_P = 0, tnw_S = 128;  // P * S = 1024 waves = one per SIMD at K = 3
+  int tnw_Smax = 128;                       // slab capacity; tnw_S is set per batch (tnw_slices)
   bool tnw_x3 = false;                     // split-bf16 weight-gradient kernel (tnwx3.hip)
   float* slabW = nullptr;
   int fin_blocks = 1;             // slabsum grid.x
@@ -647,7 +648,7 @@ int build_buffers(dbsde_ctx* c) {
   if (const char* e = getenv("DBSDE_TNW")) c->tnw = c->tnw && atoi(e) != 0;
   std::vector<PackDesc> F;
   if (c->tnw) {
-    const int T = Dp, P = 2 * K + 2, S = c->tnw_S;
+    const int T = Dp, P = 2 * K + 2, S = c->tnw_Smax;
     c->tnw_nb = T / 16;
     c->tnw_P = P;
     const char* ex = getenv("DBSDE_TNW_X3");
@@ -1846,6 +1847,26 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
   return DBSDE_OK;
 }
 
+// weight-gradient row slices for a batch of Rp rows: at least four 32-row
+// steps per slice, a multiple of 8, at most the slab capacity (128 at the
+// north star; small batches write and finalize fewer partial slabs: 48 at
+// M = 128, so the finalize reads 19 instead of 51 MB)
+int tnw_slices(const dbsde_ctx* c, int Rp) {
+  const int s = (Rp / 32 / 4) / 8 * 8;
+  return std::min(c->tnw_Smax, std::max(8, s));
+}
+
+// resident workgroups of the chip for a phase variant (two per CU for the
+// 64-row and column-split kernels, one for the 512-register ones), queried once
+int variant_slots(dbsde_ctx* c, int fv) {
+  if (c->fv_slots[fv] == 0) {
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kFused[fv].A, 64 * P3_WAVES, 0) != hipSuccess) per = 1;
+    c->fv_slots[fv] = std::max(1, per) * c->cus;
+  }
+  return c->fv_slots[fv];
+}
+
 int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, float* grad, const dbsde_outputs* out,
                    const FusedOpt* fo) {
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
@@ -1880,10 +1901,15 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   int nloss_parts;
   bool tnw_piped = false;
   FusedArgs fa;
+  c->tnw_S = tnw_slices(c, Rp);
   int fv = c->fv;
-  // small batches: the column-split kernels when the 64-row ones would fill
-  // at most half of their workgroup slots (M <= 256 at the north star)
-  if (fv >= 0 && c->fv_cs >= 0 && (c->cs_mode == 1 || Rp / P3_ROWS <= c->cus)) fv = c->fv_cs;
+  // small batches: the column-split kernels when all their 16-row workgroups
+  // are resident at once (M <= 128 per GPU at the north star); past that their
+  // 4x workgroup count costs more than the shorter chains save (M = 256:
+  // 0.235 vs 0.209 ms/step, profiles/r4_ab_column_split.txt)
+  if (fv >= 0 && c->fv_cs >= 0 &&
+      (c->cs_mode == 1 || (c->cs_mode == 2 && Rp / CS_ROWS <= variant_slots(c, c->fv_cs))))
+    fv = c->fv_cs;
   if (fv >= 0) {
     fa = fused_args(c, R, Rp, N1, q3);
     if (!fused_piece_counts_ok(c, fa)) return fail(c, DBSDE_EINVAL, "internal: fused kernel piece counts");
@@ -1897,12 +1923,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     const int WR = kFused[fv].rows;
     // workgroup slots of the chip for this variant (two per CU for the
     // 64-row kernels, one for the 512-register ones)
-    if (c->fv_slots[fv] == 0) {
-      int per = 0;
-      HIPC(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kFused[fv].A, 64 * P3_WAVES, 0));
-      c->fv_slots[fv] = std::max(1, per) * c->cus;
-    }
-    const int slots = c->fv_slots[fv];
+    const int slots = variant_slots(c, fv);
     int nch = !grad ? 1 : (c->chunks > 0 ? c->chunks : (Rp / WR > slots ? 2 : 1));
     while (nch > 1 && (M % WR != 0 || (M / WR) % nch != 0)) --nch;
     if (nch <= 1) {
@@ -2191,6 +2212,7 @@ int dbsde_net_u_vjp(dbsde_ctx* c, const float* params, int R, const float* t, co
         ext_cotan_kernel<<<nb, 256, 0, s>>>(ubar, zbar, R, Rp, D, c->Dp, c->u_clamp ? c->umask : nullptr, c->ubar,
                                             c->zbar, c->u16));
   }
+  c->tnw_S = tnw_slices(c, Rp);
   return backward_tail(c, params, R, Rp, fv, grad, nullptr, 0, nullptr, nullptr, false);
 }
 

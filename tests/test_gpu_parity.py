@@ -81,7 +81,7 @@ def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=1, cs=None):
     finally:
         for k, v in old.items():
             if v is None:
-                del os.environ[k]
+                os.environ.pop(k, None)
             else:
                 os.environ[k] = v
 

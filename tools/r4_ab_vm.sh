@@ -15,11 +15,10 @@ print(sys.argv[2], "ms/step %.4f" % d["ms_per_step"], {n: k[n] for n in list(k)[
 PY
 }
 for m in 128 256 512; do
-  for v in "X=1" "DBSDE_CS=0" "DBSDE_CS=0 DBSDE_CHUNKS=2"; do
+  for v in "X=1" "DBSDE_CS=0" "DBSDE_CS=1 DBSDE_CHUNKS=1"; do
     tag=$(echo "$v" | tr ' =' '__')
     env $v timeout -k 10 200 python bench.py --paths-per-gpu $m --no-cpu-baseline --no-parity --steps 100 > gpurun_out/ablib/m${m}_$tag.log 2>&1 || { echo fail m$m $v; tail -5 gpurun_out/ablib/m${m}_$tag.log; exit 1; }
     summ gpurun_out/ablib/m${m}_$tag.log "M=$m $v"
   done
 done
-tools/ab_libs.sh "--no-cpu-baseline --no-parity --steps 100" vm0 tnwchain > gpurun_out/ablib/bsb.txt 2>&1 || { cat gpurun_out/ablib/bsb.txt; exit 1; }
-cat gpurun_out/ablib/bsb.txt
+timeout -k 10 200 python bench.py --no-cpu-baseline --no-parity --steps 100 > gpurun_out/ablib/bsb_default.log 2>&1 && summ gpurun_out/ablib/bsb_default.log "bsb M=1024"
