@@ -212,6 +212,7 @@ __device__ __forceinline__ const float* lane_ptr(unsigned long long v, int idx) 
 template <int NBUF, int LC, int NF = 0, int NP = 0>
 struct PieceStagerT {
   static constexpr int nbuf = NBUF;
+  static constexpr bool kRegs = false;   // (phasecs.hip's register-streamed feed: true)
   floatx4* wl;
   const float* const* img;
   const int* nf;

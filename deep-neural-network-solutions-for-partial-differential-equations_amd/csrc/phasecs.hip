@@ -72,10 +72,67 @@ __device__ __forceinline__ floatx4 vec_at(const float* v, int o, int q, bool ok)
   return pick(ok, x, floatx4{0.f, 0.f, 0.f, 0.f});
 }
 
-// the layer-input exchange: own fragments in, the whole B-operand tile out
-__device__ __forceinline__ void xput(const Mat<2>& m, floatx4* xb, const Own& w, int lane) {
-  xb[w.o0 * 64 + lane] = m.v[0];
-  xb[(w.o0 + (w.n > 1 ? 1 : 0)) * 64 + lane] = pick(w.n > 1, m.v[1], m.v[0]);
+// the layer-input exchange: own fragments in, the whole B-operand tile out.
+// DBL (register-streamed weights, no per-piece barrier): two tiles used in
+// turn, so a wave that runs a stage ahead never overwrites the tile a slower
+// wave has still to read (the next write to a tile is a stage barrier later)
+template <int T, bool DBL>
+struct XEx {
+  floatx4* base;
+  int wr;
+  const floatx4* rd;
+};
+template <int T, bool DBL>
+__device__ __forceinline__ void xput(const Mat<2>& m, XEx<T, DBL>& x, const Own& w, int lane) {
+  floatx4* t = x.base + x.wr * (T * 64);
+  t[w.o0 * 64 + lane] = m.v[0];
+  t[(w.o0 + (w.n > 1 ? 1 : 0)) * 64 + lane] = pick(w.n > 1, m.v[1], m.v[0]);
+  x.rd = t;
+  if constexpr (DBL) x.wr ^= 1;
+}
+
+// register-streamed weights: each wave loads only its own two fragments of
+// each piece straight into registers, two pieces ahead (global_load_dwordx4,
+// 1 KiB per fragment chunk, coalesced); no LDS ring, no per-piece barrier --
+// the waves meet only at the stage barriers of the activation exchange.
+struct WFrag {
+  uintx4 w0[3], w1[3];
+};
+template <int NP>
+struct WStream {
+  static constexpr bool kRegs = true;
+  unsigned long long ptab;   // lane l: piece l's image (lane_ptr)
+  int st, off, f1, lane;
+  WFrag a, b;
+  __device__ __forceinline__ void fetch(WFrag& f, int k) {
+    const int kk = k < NP ? k : NP - 1;   // past the end: the last piece again (unused)
+    const uintx4* im = (const uintx4*)(lane_ptr(ptab, kk) + off);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) f.w0[p] = im[p * 64 + lane];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) f.w1[p] = im[(f1 + p) * 64 + lane];
+  }
+  __device__ __forceinline__ void init(const float* const* img, const Own& w, int ln) {
+    lane = ln;
+    st = 0;
+    off = 3 * w.o0 * 256;
+    f1 = w.f1;
+    ptab = lane < NP ? (unsigned long long)img[lane] : 0ull;
+    fetch(a, 0);
+    fetch(b, 1);
+  }
+  __device__ __forceinline__ WFrag next() {
+    const WFrag c = a;
+    a = b;
+    fetch(b, st + 2);
+    ++st;
+    return c;
+  }
+};
+// the piece count of a phase (phase.hpp PieceStager's NP)
+template <int T, int K, bool HV, int PH>
+constexpr int cs_pieces() {
+  return ((T + 1) / 2) * (PH == 0 ? 2 + 2 * K * (HV ? 2 : 1) : 1 + K * (HV ? 3 : 2));
 }
 template <int TT>
 __device__ __forceinline__ void xget(Mat<TT>& m, const floatx4* xb, int lane) {
@@ -126,6 +183,52 @@ __device__ __forceinline__ void sgemm_cs_piece(Mat<2>& acc, const Split3& s, con
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// the register-streamed piece: as sgemm_cs_piece, operands already in registers
+template <int TI, int KBN>
+__device__ __forceinline__ void sgemm_cs_regs(Mat<2>& acc, const Split3& s, const WFrag& f, const Mat<TI>& b,
+                                              uintx4 (&sn)[3]) {
+  constexpr bool NEXT = KBN < (TI + 1) / 2;
+  if constexpr (NEXT) {
+    split_pair<TI, NEXT ? KBN : 0, 0>(b, sn[0], sn[1], sn[2]);
+    split_pair<TI, NEXT ? KBN : 0, 1>(b, sn[0], sn[1], sn[2]);
+    split_pair<TI, NEXT ? KBN : 0, 2>(b, sn[0], sn[1], sn[2]);
+    split_pair<TI, NEXT ? KBN : 0, 3>(b, sn[0], sn[1], sn[2]);
+  }
+  floatx4 a = acc.v[0], c = acc.v[1];
+  a = mfma_bf(f.w0[0], s.l, a);
+  c = mfma_bf(f.w1[0], s.l, c);
+  a = mfma_bf(f.w0[0], s.m, a);
+  c = mfma_bf(f.w1[0], s.m, c);
+  a = mfma_bf(f.w0[1], s.m, a);
+  c = mfma_bf(f.w1[1], s.m, c);
+  a = mfma_bf(f.w0[1], s.h, a);
+  c = mfma_bf(f.w1[1], s.h, c);
+  a = mfma_bf(f.w0[2], s.h, a);
+  c = mfma_bf(f.w1[2], s.h, c);
+  acc.v[0] = mfma_bf(f.w0[0], s.h, a);
+  acc.v[1] = mfma_bf(f.w1[0], s.h, c);
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int TI, int KB, class SG>
+__device__ __forceinline__ void stage_csr_from(Mat<2>& acc, const Mat<TI>& b, SG& sg, const Split3& s) {
+  constexpr int NKB = (TI + 1) / 2;
+  if constexpr (KB < NKB) {
+    const WFrag f = sg.next();
+    __builtin_amdgcn_sched_barrier(0);   // the next pieces' loads issue before this piece's MFMAs
+    uintx4 sn[3];
+    sgemm_cs_regs<TI, KB + 1>(acc, s, f, b, sn);
+    if constexpr (KB + 1 < NKB)
+      stage_csr_from<TI, KB + 1>(
+          acc, b, sg,
+          Split3{__builtin_bit_cast(bf16x8, sn[0]), __builtin_bit_cast(bf16x8, sn[1]), __builtin_bit_cast(bf16x8, sn[2])});
+  }
+}
+
 template <int TI, int NPRE, int NAFTER, int KB, class SG>
 __device__ __forceinline__ void stage_cs_from(Mat<2>& acc, const Mat<TI>& b, SG& sg, int lane, const Own& w,
                                               const Split3& s) {
@@ -145,22 +248,46 @@ __device__ __forceinline__ void stage_cs_from(Mat<2>& acc, const Mat<TI>& b, SG&
 // from LDS after the first piece's barrier (which publishes it); `after` runs
 // right after that barrier (deferred stores, early loads).  NPRE / NAFTER as
 // phase.hpp stage_mm (lower bounds over the four waves).
-template <int TI, int NPRE, int NAFTER, bool XIN, class SG, class F>
-__device__ __forceinline__ void stage_cs(Mat<2>& acc, Mat<TI>& b, SG& sg, int lane, const Own& w, const floatx4* xb,
+template <int TI, int NPRE, int NAFTER, bool XIN, class SG, class X, class F>
+__device__ __forceinline__ void stage_cs(Mat<2>& acc, Mat<TI>& b, SG& sg, int lane, const Own& w, const X& xb,
                                          F&& after) {
   constexpr int NKB = (TI + 1) / 2;
-  const floatx4* wp = sg.template next<piece_nyoung<0, SG::nbuf - 1, NPRE, NAFTER>()>();
-  if constexpr (XIN) xget(b, xb, lane);
-  after();
-  __builtin_amdgcn_sched_barrier(0);
-  const Split3 s = split_block<TI, 0>(b);
-  uintx4 sn[3];
-  sgemm_cs_piece<TI, 1>(acc, s, wp + w.off, w.f1, lane, b, sn);
-  if constexpr (NKB > 1)
-    stage_cs_from<TI, NPRE, NAFTER, 1>(
-        acc, b, sg, lane, w,
-        Split3{__builtin_bit_cast(bf16x8, sn[0]), __builtin_bit_cast(bf16x8, sn[1]), __builtin_bit_cast(bf16x8, sn[2])});
+  if constexpr (SG::kRegs) {
+    if constexpr (XIN) {
+      lds_barrier();   // publishes the exchange tile (and keeps every vector-memory op in flight)
+      xget(b, xb.rd, lane);
+    }
+    after();
+    __builtin_amdgcn_sched_barrier(0);
+    stage_csr_from<TI, 0>(acc, b, sg, split_block<TI, 0>(b));
+  } else {
+    const floatx4* wp = sg.template next<piece_nyoung<0, SG::nbuf - 1, NPRE, NAFTER>()>();
+    if constexpr (XIN) xget(b, xb.rd, lane);
+    after();
+    __builtin_amdgcn_sched_barrier(0);
+    const Split3 s = split_block<TI, 0>(b);
+    uintx4 sn[3];
+    sgemm_cs_piece<TI, 1>(acc, s, wp + w.off, w.f1, lane, b, sn);
+    if constexpr (NKB > 1)
+      stage_cs_from<TI, NPRE, NAFTER, 1>(
+          acc, b, sg, lane, w,
+          Split3{__builtin_bit_cast(bf16x8, sn[0]), __builtin_bit_cast(bf16x8, sn[1]), __builtin_bit_cast(bf16x8, sn[2])});
+  }
 }
+
+#ifndef DBSDE_CS_REG
+#define DBSDE_CS_REG 1
+#endif
+// the weight feed of a phase: register-streamed (DBSDE_CS_REG=1) or the
+// 64-row kernels' LDS-DMA ring shared by the four waves
+template <bool REG, int T, int TD, int K, bool HV, int PH>
+struct FeedOf {
+  using type = PieceStager<true, T, TD, K, HV, PH>;
+};
+template <int T, int TD, int K, bool HV, int PH>
+struct FeedOf<true, T, TD, K, HV, PH> {
+  using type = WStream<cs_pieces<T, K, HV, PH>()>;
+};
 
 }  // namespace
 
@@ -171,20 +298,26 @@ __device__ __forceinline__ void stage_cs(Mat<2>& acc, Mat<TI>& b, SG& sg, int la
 template <int T, int TD, int K, int ACT, bool HV>
 __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseAcs_kernel(FusedArgs p) {
   static_assert(T == TD && T == 7, "column-split kernels: width-112 levels");
-  constexpr int BUF = 3 * T * 64;
-  // ONE __shared__ array (phase.hpp phaseC_kernel): the weight ring, the
-  // exchange tile, the cross-wave sums [4 waves][16 rows][8]
-  __shared__ floatx4 wl[P3_NBUF_X3 * BUF + T * 64 + P3_WAVES * 16 * 8 / 4];
-  floatx4* xb = wl + P3_NBUF_X3 * BUF;
-  float* red = (float*)(xb + T * 64);
+  constexpr bool REG = DBSDE_CS_REG != 0;
+  constexpr int BUF = 3 * T * 64, RING = REG ? 0 : P3_NBUF_X3 * BUF, NX = REG ? 2 : 1;
+  // ONE __shared__ array (phase.hpp phaseC_kernel): the weight ring (LDS
+  // feed), the exchange tile(s), the cross-wave sums [4 waves][16 rows][8]
+  __shared__ floatx4 wl[RING + NX * T * 64 + P3_WAVES * 16 * 8 / 4];
+  XEx<T, REG> xb{wl + RING, 0, wl + RING};
+  float* red = (float*)(wl + RING + NX * T * 64);
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Own w = own_of<T>(wave);
   const int tile = blockIdx.x + p.tile0;
   const int row0 = tile * CS_ROWS;
   const int S = p.S, Wd = p.W, c0 = 16 * w.o0;
-  PieceStager<true, T, TD, K, HV, 0> sg{wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
-  sg.start();
+  typename FeedOf<REG, T, TD, K, HV, 0>::type sg;
+  if constexpr (REG) {
+    sg.init(p.simgA, w, lane);
+  } else {
+    sg = {wl, p.simgA, p.snfA, p.nA, 0, wave, lane, BUF};
+    sg.start();
+  }
   Mat<TD> x;
   bload(x, p.xin, p.Dp, row0, 0);
 
@@ -358,17 +491,23 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseAcs_kernel(FusedArgs p)
 template <int T, int TD, int K, int ACT, bool HV>
 __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseCcs_kernel(FusedArgs p) {
   static_assert(T == TD && T == 7, "column-split kernels: width-112 levels");
-  constexpr int BUF = 3 * T * 64;
-  __shared__ floatx4 wl[P3_NBUF_X3 * BUF + T * 64];
-  floatx4* xb = wl + P3_NBUF_X3 * BUF;
+  constexpr bool REG = DBSDE_CS_REG != 0;
+  constexpr int BUF = 3 * T * 64, RING = REG ? 0 : P3_NBUF_X3 * BUF, NX = REG ? 2 : 1;
+  __shared__ floatx4 wl[RING + NX * T * 64];
+  XEx<T, REG> xb{wl + RING, 0, wl + RING};
   const int lane = threadIdx.x & 63, q = lane >> 4, cl = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Own w = own_of<T>(wave);
   const int tile = blockIdx.x + p.tile0;
   const int row0 = tile * CS_ROWS;
   const int S = p.S, Wd = p.W, c0 = 16 * w.o0;
-  PieceStager<true, T, TD, K, HV, 1> sg{wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
-  sg.start();
+  typename FeedOf<REG, T, TD, K, HV, 1>::type sg;
+  if constexpr (REG) {
+    sg.init(p.simgC, w, lane);
+  } else {
+    sg = {wl, p.simgC, p.snfC, p.nC, 0, wave, lane, BUF};
+    sg.start();
+  }
 
   // residuals and cotangents of row cl (every wave: the whole zbar tile is
   // the x-stack stages' input)

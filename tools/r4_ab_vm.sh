@@ -22,3 +22,5 @@ for m in 128 256 512; do
   done
 done
 timeout -k 10 200 python bench.py --no-cpu-baseline --no-parity --steps 100 > gpurun_out/ablib/bsb_default.log 2>&1 && summ gpurun_out/ablib/bsb_default.log "bsb M=1024"
+# column-split weight feed: registers (base) vs the shared LDS-DMA ring (csl)
+tools/ab_libs.sh "--paths-per-gpu 128 --no-cpu-baseline --no-parity --steps 100" csl > gpurun_out/ablib/csl.txt 2>&1; cat gpurun_out/ablib/csl.txt
