@@ -1847,13 +1847,14 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
   return DBSDE_OK;
 }
 
-// weight-gradient row slices for a batch of Rp rows: at least four 32-row
-// steps per slice, a multiple of 8, at most the slab capacity (128 at the
-// north star; small batches write and finalize fewer partial slabs: 48 at
-// M = 128, so the finalize reads 19 instead of 51 MB)
+// weight-gradient row slices for a batch of Rp rows.  Always the slab
+// capacity: fewer, longer slices at small batches (48 at M = 128, four 32-row
+// steps each) cut the finalize's slab reads (23.9 -> 22.4 us) but leave the
+// weight-gradient kernel with a third of the waves (33 -> 49 us,
+// profiles/r4_ab_column_split.txt)
 int tnw_slices(const dbsde_ctx* c, int Rp) {
-  const int s = (Rp / 32 / 4) / 8 * 8;
-  return std::min(c->tnw_Smax, std::max(8, s));
+  (void)Rp;
+  return c->tnw_Smax;
 }
 
 // resident workgroups of the chip for a phase variant (two per CU for the
