@@ -174,7 +174,8 @@ struct dbsde_ctx {
   // fragment images (phase.hpp) of every operand matrix: X_j = [W_in|b] / [V_j|b_j+c_j]
   // (out W, in Dp), Z_j = its transpose (out Dp, in W), F_j = B_j, Bk_j = B_j^T
   std::vector<float*> imgX, imgZ, imgF, imgB;
-  int tn_splits = 96;              // weight-gradient GEMM row splits (A/B: 64..128 best on MI355X)
+  int tn_splits = 96;              // weight-gradient GEMM row splits (A/B: 64..128 best on MI355X): slab capacity
+  int tn_splits_cur = 96;          // the splits of the last weight-gradient launch (<= tn_splits)
   // wave-owned weight-gradient tiles (tnw.hpp): NAIS layouts with Dp == Wp
   bool tnw = false;
   int tnw_nb = 0, tnw_P = 0, tnw_S = 128;  // P * S = 1024 waves = one per SIMD at K = 3
@@ -1288,7 +1289,8 @@ int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double*
         tilefin_kernel<<<dim3((T * T + TF_ELEMS - 1) / TF_ELEMS, c->tnw_P + 1), 256, 0, s>>>(
             c->d_fin, c->n_fin, c->slabW, c->tnw_S, c->tnw_P, T, grad, loss_part, nloss, loss, f, fuse));
   } else {
-    RUN(c, "grad_finalize", 0.0, 0.0, slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad));
+    RUN(c, "grad_finalize", 0.0, 0.0,
+        slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad, c->tn_splits_cur));
   }
   if (c->proj) {
     const int LW = c->L[1];
@@ -1745,7 +1747,11 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
   } else {
   TNArgs ta;
   memset(&ta, 0, sizeof(ta));
-  const int S_ = c->tn_splits;
+  // row splits for this batch: at least 16 32-row steps each, at most the
+  // slab capacity (fewer partial slabs to write and finalize at small batches;
+  // every kernel below covers all S_ splits, empty ones writing zeros, and the
+  // finalize sums exactly S_ of them)
+  const int S_ = c->tn_splits_cur = std::min(c->tn_splits, std::max(8, (Rp + 511) / 512));
   const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
   ta.rows_per_split = rps;
   ta.Rp = Rp;
@@ -1837,7 +1843,7 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
     TNArgs to = ta;
     to.prob[0] = ta.prob[K + 1];
     RUN(c, "tn_weight_grad", tfl, 0.0,
-        tn_x3_kernel<<<dim3(maxt3, (Rp + rps32 - 1) / rps32, K + 1), 256, 0, s>>>(ta, rps32);
+        tn_x3_kernel<<<dim3(maxt3, S_, K + 1), 256, 0, s>>>(ta, rps32);
         tn_gemm_kernel<<<dim3(ta.prob[K + 1].mt * ta.prob[K + 1].nt, S_, 1), 256, 0, s>>>(to));
   } else {
     RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));

@@ -898,8 +898,11 @@ __global__ void __launch_bounds__(256) netu_input_kernel(const float* t, const f
 // 64 elements per block, the slabs split over 4 thread groups whose fp64
 // partials are added in a fixed order.
 #ifndef DBSDE_DEVICE_HELPERS_ONLY
-__global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, float* grad) {
-  const PackDesc& d = descs[blockIdx.y];
+// nslab: the slabs the weight-gradient launch wrote (its row splits); a
+// descriptor's own nslab is the capacity (0: a zero window)
+__global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, float* grad, int nslab) {
+  PackDesc d = descs[blockIdx.y];
+  if (d.nslab > 0) d.nslab = nslab;
   const int total = d.rows * d.cols;
   if ((int)blockIdx.x * 64 >= total) return;
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
