@@ -261,3 +261,33 @@ def test_phase_chunk_count_does_not_change_the_step(pkg, dev, M):
     for ch in ("2", None):
         torch.testing.assert_close(res[ch][0], res["1"][0], rtol=0, atol=0)
         torch.testing.assert_close(res[ch][1], res["1"][1], rtol=0, atol=0)
+
+
+def test_weight_gradient_splits_follow_the_batch(pkg, dev):
+    """The chain / width-256 weight-gradient tiles split the rows per batch
+    (at least 16 32-row steps per split) and the finalize sums exactly the
+    splits written: a step at a small batch after one at a large batch on the
+    same context gives the fresh context's gradient bit for bit (no partial
+    slab of the larger batch leaks in)."""
+    from test_gpu_parity import make_solver
+    g = _load("g1_w256_hjb_FC_Sine_N20.npz")
+    layers = [int(v) for v in g["layers"]]
+    D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
+    params = torch.from_numpy(g["params"]).to(dev)
+    xi = torch.from_numpy(g["Xi"]).to(dev).contiguous()
+
+    def small(s):
+        grad, loss = torch.empty_like(params), torch.empty(1, device=dev)
+        s.loss_grad(params, M, N, xi, t=torch.from_numpy(g["t"]).to(dev).reshape(M, N + 1).contiguous(),
+                    W=torch.from_numpy(g["W"]).to(dev).contiguous(), grad=grad, loss=loss)
+        torch.cuda.synchronize()
+        return grad.cpu(), loss.cpu()
+
+    a = make_solver(pkg, dev, g)
+    big = 2048
+    gb, lb = torch.empty_like(params), torch.empty(1, device=dev)
+    a.loss_grad(params, big, N, xi, seed=3, grad=gb, loss=lb)
+    ga, la = small(a)
+    gf, lf = small(make_solver(pkg, dev, g))
+    torch.testing.assert_close(la, lf, rtol=0, atol=0)
+    torch.testing.assert_close(ga, gf, rtol=0, atol=0)

@@ -2,7 +2,7 @@
 # Round-4 rocprofv3 stats + counter passes for the other BASELINE workloads and
 # the M=128 strong-scaling shape (tools/profile_round.sh each)
 mkdir -p gpurun_out/prof4
-timeout -k 10 300 python -u -m pytest tests/test_gpu_round4.py tests/test_gpu_parity.py -q --timeout 120 --timeout-method thread -k "w256 or hjb or oned or chunk" > gpurun_out/prof4/tests.txt 2>&1; tail -3 gpurun_out/prof4/tests.txt
+timeout -k 10 300 python -u -m pytest tests/test_gpu_round4.py tests/test_gpu_parity.py -q --timeout 120 --timeout-method thread -k "w256 or hjb or oned or chunk or splits" > gpurun_out/prof4/tests.txt 2>&1; tail -3 gpurun_out/prof4/tests.txt
 timeout -k 10 200 python bench.py --workload oned --no-cpu-baseline --no-parity --steps 50 > gpurun_out/prof4/oned.log 2>&1 && tail -c 300 gpurun_out/prof4/oned.log
 tools/profile_round.sh r4 basket || exit $?
 tools/profile_round.sh r4 heston || exit $?
