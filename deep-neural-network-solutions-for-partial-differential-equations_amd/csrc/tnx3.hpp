@@ -65,6 +65,9 @@ __device__ __forceinline__ void tx3_store(const TnX3Step& s, uintx4* img) {
 }
 
 // grid (tiles_m * tiles_n, splits, problems); rps = rows per split (multiple of 32)
+#ifndef DBSDE_TNX3_PD
+#define DBSDE_TNX3_PD 2
+#endif
 #ifndef DBSDE_TNX3_XCD
 #define DBSDE_TNX3_XCD 1
 #endif
@@ -72,7 +75,7 @@ __device__ __forceinline__ void tx3_store(const TnX3Step& s, uintx4* img) {
 // eight contiguous runs of (tile, split, problem), one per XCD -- the tiles of
 // one split, which share their A / B column strips, run together on one XCD
 // and read the strips once into its L2 instead of once per tile.
-__global__ void __launch_bounds__(256) tn_x3_kernel(TNArgs args, int rps) {
+__global__ void __launch_bounds__(256, 2) tn_x3_kernel(TNArgs args, int rps) {
   const int nx = gridDim.x, ny = gridDim.y;
   int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
   const int per = nx * ny * gridDim.z / 8;
@@ -97,15 +100,18 @@ __global__ void __launch_bounds__(256) tn_x3_kernel(TNArgs args, int rps) {
     for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
   float bsum[2] = {0.f, 0.f};
   const int total = nstep * P.npairs;
-  TnX3Step ra, rb;
-  auto load = [&](int it) __attribute__((always_inline)) {
+  // global loads DBSDE_TNX3_PD steps ahead: with two register sets a step's
+  // strips have two steps of MFMA time to arrive from HBM (the loop is
+  // unrolled by two so each set is named statically)
+  TnX3Step ra0, rb0, ra1, rb1;
+  auto load = [&](TnX3Step& a, TnX3Step& b, int it) __attribute__((always_inline)) {
     const int pr = it / nstep, st = it - pr * nstep;
     const int r0 = r_begin + 32 * st;
-    tx3_load(ra, P.A[pr], P.lda[pr], P.nA[pr], TX_TILE * tm, r0);
-    tx3_load(rb, P.B[pr], P.ldb[pr], P.nB[pr], TX_TILE * tn, r0);
+    tx3_load(a, P.A[pr], P.lda[pr], P.nA[pr], TX_TILE * tm, r0);
+    tx3_load(b, P.B[pr], P.ldb[pr], P.nB[pr], TX_TILE * tn, r0);
   };
-  if (total > 0) load(0);
-  for (int it = 0; it < total; ++it) {
+  constexpr int PD = DBSDE_TNX3_PD;
+  auto step = [&](TnX3Step& ra, TnX3Step& rb, TnX3Step& na, TnX3Step& nb, int it) __attribute__((always_inline)) {
     if (bias && it < nstep) {   // pair 0: fixed row order within the thread
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -115,7 +121,9 @@ __global__ void __launch_bounds__(256) tn_x3_kernel(TNArgs args, int rps) {
     tx3_store(ra, sa);
     tx3_store(rb, sb);
     __syncthreads();
-    if (it + 1 < total) load(it + 1);
+    // PD 2: step it + 2 into this step's (now stored) registers; PD 1: it + 1
+    // into the same set
+    if (it + PD < total) load(PD == 2 ? ra : na, PD == 2 ? rb : nb, it + PD);
     uintx4 fb[4][3];
 #pragma unroll
     for (int n = 0; n < 4; ++n)
@@ -139,6 +147,17 @@ __global__ void __launch_bounds__(256) tn_x3_kernel(TNArgs args, int rps) {
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a6[k], __builtin_bit_cast(bf16x8, fb[n][bp[k]]), acc[m][n], 0, 0, 0);
     }
     __syncthreads();
+  };
+  if (PD == 2) {
+    if (total > 0) load(ra0, rb0, 0);
+    if (total > 1) load(ra1, rb1, 1);
+    for (int it = 0; it < total; it += 2) {
+      step(ra0, rb0, ra0, rb0, it);
+      if (it + 1 < total) step(ra1, rb1, ra1, rb1, it + 1);
+    }
+  } else {
+    if (total > 0) load(ra0, rb0, 0);
+    for (int it = 0; it < total; ++it) step(ra0, rb0, ra0, rb0, it);
   }
   const int ldo = P.nt * 64, nrows = P.mt * 64;
   float* out = P.slab + (size_t)split * nrows * ldo;
