@@ -27,6 +27,11 @@
 #include "phase.hpp"
 #include "phase2.hpp"
 #include "phasecs.hpp"
+
+// minimum rows per weight-gradient row split of the chain layouts
+#ifndef DBSDE_TN_SPLIT_ROWS
+#define DBSDE_TN_SPLIT_ROWS 128
+#endif
 #include "chainx3.hpp"
 #include "tnx3.hpp"
 #include "tnw.hpp"
@@ -1752,7 +1757,8 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
   // 0.144 ms for the tiles against 0.017 vs 0.040 ms saved in the finalize);
   // every kernel below covers all S_ splits, empty ones writing zeros, and the
   // finalize sums exactly S_ of them
-  const int S_ = c->tn_splits_cur = std::min(c->tn_splits, std::max(8, (Rp + 127) / 128));
+  const int S_ = c->tn_splits_cur =
+      std::min(c->tn_splits, std::max(8, (Rp + DBSDE_TN_SPLIT_ROWS - 1) / DBSDE_TN_SPLIT_ROWS));
   const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
   ta.rows_per_split = rps;
   ta.Rp = Rp;
@@ -1834,18 +1840,20 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
   }
   if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
   if (c->tnx3) {
-    // split-bf16 tiles for the layer problems (tnx3.hpp), the fp32 kernel
-    // for the one-row output layer
+    // split-bf16 tiles for the layer problems (tnx3.hpp), a GEMV over the
+    // level-K tiles for the one-row output layer (tn_out_kernel; the fp32
+    // 64x64-tile GEMM took 58 us of HJB's 357)
     int maxt3 = 0;
     for (int j = 0; j <= K; ++j)
       maxt3 = std::max(maxt3, ((ta.prob[j].nA[0] + TX_TILE - 1) / TX_TILE) * ((ta.prob[j].nB[0] + TX_TILE - 1) / TX_TILE));
     const int rps32 = ((Rp + S_ - 1) / S_ + 31) / 32 * 32;
-    if (Rp % 32 != 0) return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
-    TNArgs to = ta;
-    to.prob[0] = ta.prob[K + 1];
+    if (Rp % 32 != 0 || c->Wp[K] % 4 != 0) return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
+    const TNProb& po = ta.prob[K + 1];
+    const long long sstride = (long long)po.mt * 64 * po.nt * 64;
     RUN(c, "tn_weight_grad", tfl, 0.0,
         tn_x3_kernel<<<dim3(maxt3, S_, K + 1), 256, 0, s>>>(ta, rps32);
-        tn_gemm_kernel<<<dim3(ta.prob[K + 1].mt * ta.prob[K + 1].nt, S_, 1), 256, 0, s>>>(to));
+        tn_out_kernel<<<dim3(S_, (c->Wp[K] + 255) / 256), 1024, 0, s>>>(c->u16, c->H + c->col[K], c->Hdot + c->col[K],
+                                                                         S, c->Wp[K], R, rps32, po.slab, sstride));
   } else {
     RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
   }

@@ -898,6 +898,71 @@ __global__ void __launch_bounds__(256) netu_input_kernel(const float* t, const f
 // 64 elements per block, the slabs split over 4 thread groups whose fp64
 // partials are added in a fixed order.
 #ifndef DBSDE_DEVICE_HELPERS_ONLY
+// Output-layer weight gradient of the chain layouts (u = h_K . w_out + b_out,
+// loss.backward, DeepBSDE.py:279): for row split s (rows [s rps, (s+1) rps)
+// of the R valid rows), row 0 of slab s = [sum_r ubar_r h_K[r] + hdot_K[r] |
+// sum_r ubar_r] -- the [w_out | b_out] window the finalize reads.  A GEMV
+// over the two level-K tiles, HBM-bound: 1024 threads = 16 row phases x 64
+// float4 column groups (a wave reads whole 1 KB rows), 8 rows in flight per
+// thread, the phases combined in a fixed order.  grid (splits, ceil(W / 256)).
+__global__ void __launch_bounds__(1024) tn_out_kernel(const float* u16, const float* H, const float* Hd, int ld,
+                                                      int W, int R, int rps, float* slab, long long sstride) {
+  const int s = blockIdx.x, t = threadIdx.x, cg = t & 63, ph = t >> 6;
+  const int c = blockIdx.y * 256 + 4 * cg;
+  const bool cin = c < W;   // W % 4 == 0
+  const int r0 = s * rps, r1 = min(r0 + rps, R);
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  for (int rb = r0 + ph; rb < r1; rb += 16 * 8) {
+    floatx4 h[8], hd[8];
+    float ub[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = rb + 16 * u;
+      const bool ok = r < r1 && cin;
+      const size_t o = (size_t)(ok ? r : r0) * ld + (cin ? c : 0);
+      h[u] = *(const floatx4*)(H + o);
+      hd[u] = *(const floatx4*)(Hd + o);
+      ub[u] = r < r1 ? u16[(size_t)r * 16] : 0.f;
+      if (!ok) {
+        h[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+        hd[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += ub[u] * h[u][e] + hd[u][e];
+      bsum += ub[u];
+    }
+  }
+  __shared__ floatx4 part[16][64];
+  __shared__ float bpart[16];
+  part[ph][cg] = acc;
+  if (cg == 0) bpart[ph] = bsum;
+  __syncthreads();
+  if (ph != 0) return;
+  floatx4 v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = part[k][cg];
+#pragma unroll
+  for (int h = 1; h < 16; h <<= 1)
+#pragma unroll
+    for (int k = 0; k + h < 16; k += 2 * h) v[k] += v[k + h];
+  float* row = slab + (size_t)s * sstride;
+  if (cin) *(floatx4*)(row + c) = v[0];
+  if (blockIdx.y == 0 && cg == 0) {
+    float b[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b[k] = bpart[k];
+#pragma unroll
+    for (int h = 1; h < 16; h <<= 1)
+#pragma unroll
+      for (int k = 0; k + h < 16; k += 2 * h) b[k] += b[k + h];
+    row[W] = b[0];
+  }
+}
+
 // nslab: the slabs the weight-gradient launch wrote (its row splits); a
 // descriptor's own nslab is the capacity (0: a zero window)
 __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, float* grad, int nslab) {

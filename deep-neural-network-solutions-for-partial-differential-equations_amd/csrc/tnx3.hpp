@@ -65,8 +65,11 @@ __device__ __forceinline__ void tx3_store(const TnX3Step& s, uintx4* img) {
 }
 
 // grid (tiles_m * tiles_n, splits, problems); rps = rows per split (multiple of 32)
+// loads one (1) or two (2) steps ahead: measured equal on HJB and config 1
+// (1.244 vs 1.238-1.247 ms, 0.492-0.499 vs 0.489-0.498 ms), 1 keeps the
+// kernel at 184 registers
 #ifndef DBSDE_TNX3_PD
-#define DBSDE_TNX3_PD 2
+#define DBSDE_TNX3_PD 1
 #endif
 #ifndef DBSDE_TNX3_XCD
 #define DBSDE_TNX3_XCD 1
