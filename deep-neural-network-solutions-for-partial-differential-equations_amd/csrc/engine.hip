@@ -28,9 +28,13 @@
 #include "phase2.hpp"
 #include "phasecs.hpp"
 
-// minimum rows per weight-gradient row split of the chain layouts
+// minimum rows per weight-gradient row split of the chain layouts: 448 keeps
+// HJB's 43,008 rows at the 96-split capacity (1.222-1.232 ms/step against
+// 1.244-1.250 with 84 splits) and gives config 1's 13,056 rows 30 splits
+// (0.457-0.465 against 0.483-0.494 ms with 96: a third of the finalize reads),
+// profiles/r4_ab_tn_splits.txt
 #ifndef DBSDE_TN_SPLIT_ROWS
-#define DBSDE_TN_SPLIT_ROWS 128
+#define DBSDE_TN_SPLIT_ROWS 448
 #endif
 #include "chainx3.hpp"
 #include "tnx3.hpp"
@@ -1752,11 +1756,9 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
   } else {
   TNArgs ta;
   memset(&ta, 0, sizeof(ta));
-  // row splits for this batch: at least four 32-row steps each, at most the
-  // slab capacity (16 steps each measured slower for config 1: 0.175 vs
-  // 0.144 ms for the tiles against 0.017 vs 0.040 ms saved in the finalize);
-  // every kernel below covers all S_ splits, empty ones writing zeros, and the
-  // finalize sums exactly S_ of them
+  // row splits for this batch: at least DBSDE_TN_SPLIT_ROWS rows each, at
+  // most the slab capacity; every kernel below covers all S_ splits, empty
+  // ones writing zeros, and the finalize sums exactly S_ of them
   const int S_ = c->tn_splits_cur =
       std::min(c->tn_splits, std::max(8, (Rp + DBSDE_TN_SPLIT_ROWS - 1) / DBSDE_TN_SPLIT_ROWS));
   const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
