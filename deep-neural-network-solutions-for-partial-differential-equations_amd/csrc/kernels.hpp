@@ -979,17 +979,16 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
     cc = e - r * d.cols;
     const float* src = d.src + (size_t)r * d.src_ld + cc;
     const int k0 = grp * d.nslab / 4, k1 = (grp + 1) * d.nslab / 4;
-    // 32 slabs per round, all loads in flight before the (fixed-order) sum
+    // 8 slabs per round, all loads in flight before the (fixed-order) sum: a
+    // wave's share is 2-24 slabs, so a 32-slab round never ran and the tail
+    // loop left one load in flight at a time
     int k = k0;
-    for (; k + 32 <= k1; k += 32) {
-      float x[32];
+    for (; k + 8 <= k1; k += 8) {
+      float x[8];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) x[u] = src[(size_t)(k + u) * d.slab_stride];
-      double q[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        q[u] = ((double)x[4 * u] + (double)x[4 * u + 1]) + ((double)x[4 * u + 2] + (double)x[4 * u + 3]);
-      s += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+      for (int u = 0; u < 8; ++u) x[u] = src[(size_t)(k + u) * d.slab_stride];
+      s += (((double)x[0] + (double)x[1]) + ((double)x[2] + (double)x[3])) +
+           (((double)x[4] + (double)x[5]) + ((double)x[6] + (double)x[7]));
     }
     for (; k < k1; ++k) s += src[(size_t)k * d.slab_stride];
   }
