@@ -1094,40 +1094,42 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
     }
   }
   __shared__ double part[4][4][64];
+  __shared__ double dps[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) part[grp][c][lane] = s4[c];
   __syncthreads();
-  if (grp != 0) return;
+  // wave grp scatters (and updates) component grp of the lane's four
+  // columns: the four waves' optimizer read-modify-writes run side by side
+  // instead of four dependent rounds in one wave
   double dp = 0.0;
   const PackDesc* dotd = nullptr;
   const int nwin = nwin_s;
   if (e0 < TT) {
-    const int r = e0 / T, c00 = e0 - r * T;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double v = (part[0][c][lane] + part[1][c][lane]) + (part[2][c][lane] + part[3][c][lane]);
-      const int cc = c00 + c;
-      for (int i = 0; i < nwin; ++i) {
-        const PackDesc& d = wins[i];
-        const int rr = r - d.sr0, ck = cc - d.sc0;
-        if (rr < 0 || rr >= d.rows || ck < 0 || ck >= d.cols) continue;
-        const float fv = d.scale * (float)v;
-        uintptr_t dv = (uintptr_t)d.dst;
-        const bool to_grad = dv & ((uintptr_t)1 << 61);
-        float* dst = to_grad ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
-        const size_t off = d.transpose ? (size_t)ck * d.dst_ld + rr : (size_t)rr * d.dst_ld + ck;
-        dst[off] = fv;
-        if (fuse && to_grad) opt_update(fo.a, (dst - grad) + (long long)off, fv, fo.prm, fo.m, fo.v);
-        if (d.dotR) dp += (double)fv * (double)d.dotR[(size_t)rr * d.dst_ld + ck];
-      }
+    const int r = e0 / T, c00 = e0 - r * T, c = grp;
+    const double v = (part[0][c][lane] + part[1][c][lane]) + (part[2][c][lane] + part[3][c][lane]);
+    const int cc = c00 + c;
+    for (int i = 0; i < nwin; ++i) {
+      const PackDesc& d = wins[i];
+      const int rr = r - d.sr0, ck = cc - d.sc0;
+      if (rr < 0 || rr >= d.rows || ck < 0 || ck >= d.cols) continue;
+      const float fv = d.scale * (float)v;
+      uintptr_t dv = (uintptr_t)d.dst;
+      const bool to_grad = dv & ((uintptr_t)1 << 61);
+      float* dst = to_grad ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
+      const size_t off = d.transpose ? (size_t)ck * d.dst_ld + rr : (size_t)rr * d.dst_ld + ck;
+      dst[off] = fv;
+      if (fuse && to_grad) opt_update(fo.a, (dst - grad) + (long long)off, fv, fo.prm, fo.m, fo.v);
+      if (d.dotR) dp += (double)fv * (double)d.dotR[(size_t)rr * d.dst_ld + ck];
     }
   }
   for (int i = 0; i < nwin; ++i)
     if (wins[i].dotR) dotd = &wins[i];
-  if (dotd) {   // fixed-order wave reduction of the block's <Abar, R> partial
+  if (dotd) {   // the block's <Abar, R> partial: each wave's sum, then the waves in order
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) dp += __shfl_xor(dp, o);
-    if (lane == 0) dotd->dot_part[blockIdx.x] = dp;
+    if (lane == 0) dps[grp] = dp;
+    __syncthreads();
+    if (threadIdx.x == 0) dotd->dot_part[blockIdx.x] = (dps[0] + dps[1]) + (dps[2] + dps[3]);
   }
 }
 #endif

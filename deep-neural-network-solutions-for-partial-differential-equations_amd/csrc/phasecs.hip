@@ -98,12 +98,16 @@ __device__ __forceinline__ void xput(const Mat<2>& m, XEx<T, DBL>& x, const Own&
 struct WFrag {
   uintx4 w0[3], w1[3];
 };
+#ifndef DBSDE_CS_DEPTH
+#define DBSDE_CS_DEPTH 2
+#endif
 template <int NP>
 struct WStream {
   static constexpr bool kRegs = true;
+  static constexpr int DEPTH = DBSDE_CS_DEPTH;   // pieces in flight (2 or 3)
   unsigned long long ptab;   // lane l: piece l's image (lane_ptr)
   int st, off, f1, lane;
-  WFrag a, b;
+  WFrag a, b, c2;
   __device__ __forceinline__ void fetch(WFrag& f, int k) {
     const int kk = k < NP ? k : NP - 1;   // past the end: the last piece again (unused)
     const uintx4* im = (const uintx4*)(lane_ptr(ptab, kk) + off);
@@ -120,11 +124,17 @@ struct WStream {
     ptab = lane < NP ? (unsigned long long)img[lane] : 0ull;
     fetch(a, 0);
     fetch(b, 1);
+    if constexpr (DEPTH == 3) fetch(c2, 2);
   }
   __device__ __forceinline__ WFrag next() {
     const WFrag c = a;
     a = b;
-    fetch(b, st + 2);
+    if constexpr (DEPTH == 3) {
+      b = c2;
+      fetch(c2, st + 3);
+    } else {
+      fetch(b, st + 2);
+    }
     ++st;
     return c;
   }
