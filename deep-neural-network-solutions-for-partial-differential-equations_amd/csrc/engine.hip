@@ -1133,7 +1133,6 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* const* 
                                                             const double* proj_part, int proj_n, const double* dot_part,
                                                             int dot_nblk, int dot_nused, float* grad, FusedOpt fo,
                                                             int fuse) {
-  if (fuse) fused_opt_prologue(fo, false);
   __shared__ float As[16][NAIS_LMAX + 1];   // As[r][k] = W[16 ti + r][k]
   __shared__ float Bs[NAIS_LMAX][17];       // Bs[k][c] = S[k][16 tj + c], S = Rbar + Rbar^T
   __shared__ double dot_s, nrm_s;
@@ -1159,6 +1158,8 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* const* 
     abs_[u] = ok ? Ab[k * L + cb] + Ab[cb * L + k] : 0.f;
     rs[u] = ok ? R[k * L + cb] + R[cb * L + k] : 0.f;
   }
+  // the optimizer scalars while the operand loads are in flight
+  if (fuse) fused_opt_prologue(fo, false);
   if (threadIdx.x < 64) {   // <Abar_j, R_j> from the finalize partials, fixed-order butterfly
     double dsum = 0.0;
     for (int b = threadIdx.x; b < dot_nused; b += 64) dsum += dot_part[(size_t)j * dot_nblk + b];

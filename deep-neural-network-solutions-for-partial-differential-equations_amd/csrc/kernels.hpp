@@ -1028,8 +1028,8 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
                                                       int P, int T, float* grad, const double* loss_part, int nloss,
                                                       float* loss, FusedOpt fo, int fuse) {
   const int p = blockIdx.y;
-  if (fuse) fused_opt_prologue(fo, p == P && blockIdx.x == 0);
   if (p == P) {   // zero windows (NAIS-Net's never-used input_layers[K])
+    if (fuse) fused_opt_prologue(fo, blockIdx.x == 0);
     // and, in block 0, the loss sum (loss_final_kernel's fixed order: one
     // launch fewer on the step's critical path)
     if (loss && blockIdx.x == 0) {
@@ -1093,6 +1093,9 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
       for (int c = 0; c < 4; ++c) s4[c] += (double)x[c];
     }
   }
+  // the optimizer scalars after the slab loads are in flight (its global
+  // load and barrier overlap them)
+  if (fuse) fused_opt_prologue(fo, false);
   __shared__ double part[4][4][64];
   __shared__ double dps[4];
 #pragma unroll
