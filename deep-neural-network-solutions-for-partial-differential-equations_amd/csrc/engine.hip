@@ -148,8 +148,6 @@ struct dbsde_ctx {
   unsigned char* d_used = nullptr;
   PackDesc* d_prep = nullptr;
   int n_prep = 0;
-  int *d_negproj = nullptr, *d_negproj_of = nullptr;   // rtr_pack_kernel: projected descriptors
-  unsigned* d_rtr_cnt = nullptr;                        // rtr_pack_kernel: finished tiles per NAIS block
 
   int prep_blocks = 1;   // pack_tagged_kernel grid.x: one element per thread
   PackDesc* d_fin = nullptr;
@@ -621,7 +619,6 @@ int build_buffers(dbsde_ctx* c) {
     P.push_back(frag(mk_desc(ptag(w.w), D + 1, c->BtZ + c->col[j], c->Stot_x, w.out, D + 1, 1, PK_COPY), c->imgZ[j],
                      TW, TDp, 0, 0));
   };
-  std::vector<int> negproj_of;   // the two projected-image descriptors of each NAIS block
   add_x_level(0, c->in, nullptr);
   if (c->has_v)
     for (int j = 1; j <= K; ++j) add_x_level(j, c->V[j - 1], &c->B[j - 1]);
@@ -634,13 +631,11 @@ int build_buffers(dbsde_ctx* c) {
       d.proj_n = nblk;
       d.proj_norm = c->norms + (j - 1);
       P.push_back(frag(d, c->imgF[j], TW, TW, 0, 0));
-      negproj_of.push_back((int)P.size() - 1);
       d = mk_desc(c->rtr[j], LW, c->Bb[j], c->Wp[j], LW, LW, 1, PK_NEGPROJ);
       d.proj = c->proj_part + (size_t)(j - 1) * nblk;
       d.proj_n = nblk;
       d.proj_norm = nullptr;
       P.push_back(frag(d, c->imgB[j], TW, TW, 0, 0));
-      negproj_of.push_back((int)P.size() - 1);
     } else {
       P.push_back(frag(mk_desc(ptag(b.w), b.in, c->Bf[j], c->Wp[j - 1], b.out, b.in, 0, PK_COPY), c->imgF[j], TW,
                        TW, 0, 0));
@@ -769,16 +764,6 @@ int build_buffers(dbsde_ctx* c) {
   // descriptors are stored with tagged pointers; the kernel arguments carry the
   // real params/grad bases (pack_kernel_tagged below).
   HIPC(c, hipMemcpy(c->d_prep, P.data(), P.size() * sizeof(PackDesc), hipMemcpyHostToDevice));
-  if (c->proj) {   // rtr_pack_kernel's tables and per-block counters
-    std::vector<int> neg(P.size(), 0);
-    for (int i : negproj_of) neg[i] = 1;
-    if ((rc = dalloc_t(c, &c->d_negproj, neg.size()))) return rc;
-    if ((rc = dalloc_t(c, &c->d_negproj_of, negproj_of.size()))) return rc;
-    if ((rc = dalloc_t(c, &c->d_rtr_cnt, (size_t)K))) return rc;
-    HIPC(c, hipMemcpy(c->d_negproj, neg.data(), neg.size() * sizeof(int), hipMemcpyHostToDevice));
-    HIPC(c, hipMemcpy(c->d_negproj_of, negproj_of.data(), negproj_of.size() * sizeof(int), hipMemcpyHostToDevice));
-    HIPC(c, hipMemset(c->d_rtr_cnt, 0, (size_t)K * sizeof(unsigned)));
-  }
   HIPC(c, hipMemcpy(c->d_fin, F.data(), F.size() * sizeof(PackDesc), hipMemcpyHostToDevice));
   return DBSDE_OK;
 }
@@ -1012,16 +997,13 @@ __device__ __forceinline__ const float* untag(const float* p, const float* param
   if (v & ((uintptr_t)1 << 61)) return grad + ((v & (((uintptr_t)1 << 61) - 1)) >> 2);
   return p;
 }
-// descriptor di packed by block blk of nblk (elements blk * 256 + t, stride
-// nblk * 256)
-__device__ __forceinline__ void pack_block(const PackDesc* descs, int di, const float* params, float* grad,
-                                           int blk, int nblk) {
+__device__ __forceinline__ void pack_block(const PackDesc* descs, int di, const float* params, float* grad) {
   PackDesc d = descs[di];
   d.src = untag(d.src, params, grad);
   d.src2 = untag(d.src2, params, grad);
   d.dst = (float*)untag(d.dst, params, grad);
   const int total = d.rows * d.cols;
-  if (blk * 256 >= total) return;
+  if ((int)blockIdx.x * 256 >= total) return;
   // NAIS projection: |RtR|_F from rtr_params_kernel's partials (fixed order)
   __shared__ float nrm_s;
   if (d.mode == PK_NEGPROJ) {
@@ -1033,12 +1015,12 @@ __device__ __forceinline__ void pack_block(const PackDesc* descs, int di, const 
       if (threadIdx.x == 0) {
         const double n = sqrt(sq);
         nrm_s = (float)n;
-        if (blk == 0 && d.proj_norm) *d.proj_norm = n;
+        if (blockIdx.x == 0 && d.proj_norm) *d.proj_norm = n;
       }
     }
     __syncthreads();
   }
-  for (int i = blk * 256 + threadIdx.x; i < total; i += nblk * 256) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int r = i / d.cols, cc = i - r * d.cols;
     float v;
     if (d.mode == PK_COPY) {
@@ -1091,7 +1073,7 @@ __device__ __forceinline__ void pack_block(const PackDesc* descs, int di, const 
   }
 }
 __global__ void __launch_bounds__(256) pack_tagged_kernel(const PackDesc* descs, const float* params, float* grad) {
-  pack_block(descs, blockIdx.y, params, grad, blockIdx.x, gridDim.x);
+  pack_block(descs, blockIdx.y, params, grad);
 }
 // RtR_j = W_j^T W_j (Functions/naisnet.py:33) and per-tile partial sums of
 // squares for the Frobenius norm (fixed order).  One 16x16 output tile per
@@ -1137,35 +1119,6 @@ __device__ __forceinline__ void rtr_tile(const float* params, const long long* w
 __global__ void __launch_bounds__(256) rtr_params_kernel(const float* params, const long long* woffs, int L,
                                                          float* const* rtr, float* const* wsnap, double* part, int nblk) {
   rtr_tile(params, woffs, L, rtr, wsnap, part, nblk, blockIdx.y, blockIdx.x);
-}
-// RtR tiles and the weight packing in one launch: rows y < K of the grid are
-// the RtR tiles of block j = y; the block that completes block j's last tile
-// (a per-block counter, released and acquired with device-scope fences)
-// packs j's two projected images (they need all of RtR_j and its norm); rows
-// y >= K pack the other descriptors (negproj[i] marks the projected ones,
-// skipped there).  No block waits on another, so no co-residency is assumed.
-__global__ void __launch_bounds__(256) rtr_pack_kernel(const float* params, const long long* woffs, int L,
-                                                       float* const* rtr, float* const* wsnap, double* part, int nblk,
-                                                       int K, const PackDesc* descs, const int* negproj,
-                                                       const int* negproj_of, unsigned* cnt) {
-  const int y = blockIdx.y;
-  if (y >= K) {
-    const int di = y - K;
-    if (!negproj[di]) pack_block(descs, di, params, nullptr, blockIdx.x, gridDim.x);
-    return;
-  }
-  if ((int)blockIdx.x >= nblk) return;
-  rtr_tile(params, woffs, L, rtr, wsnap, part, nblk, y, blockIdx.x);
-  __shared__ unsigned last_s;
-  __threadfence();   // this tile and its partial, visible device-wide
-  __syncthreads();
-  if (threadIdx.x == 0) last_s = atomicAdd(cnt + y, 1u) == (unsigned)nblk - 1u;
-  __syncthreads();
-  if (!last_s) return;
-  __threadfence();   // every other tile of block y, visible here
-  pack_block(descs, negproj_of[2 * y], params, nullptr, 0, 1);
-  pack_block(descs, negproj_of[2 * y + 1], params, nullptr, 0, 1);
-  if (threadIdx.x == 0) cnt[y] = 0u;   // for the next step (the launch boundary orders it)
 }
 // NAIS projection adjoint (Functions/naisnet.py:30-39 reversed), one kernel:
 //   Abar_j = dL/dA_j (slab sums), R_j = W_j^T W_j, n = |R_j|_F
@@ -1252,14 +1205,12 @@ namespace {
 int prep_weights(dbsde_ctx* c, const float* params) {
   hipStream_t s = c->stream;
   const int LW = c->L[1];
-  if (c->proj) {   // RtR, its norm and every fragment image in one launch
+  if (c->proj) {
     const double fl = 2.0 * c->K * LW * (double)LW * LW;
     const int nblk = ((LW + 15) / 16) * ((LW + 15) / 16);
-    RUN(c, "rtr_pack", fl, 0.0,
-        rtr_pack_kernel<<<dim3(std::max(nblk, c->prep_blocks), c->K + c->n_prep), 256, 0, s>>>(
-            params, c->d_woffs, LW, c->d_rtr, c->d_wsnap, c->proj_part, nblk, c->K, c->d_prep, c->d_negproj,
-            c->d_negproj_of, c->d_rtr_cnt));
-    return DBSDE_OK;
+    RUN(c, "rtr", fl, 0.0,
+        rtr_params_kernel<<<dim3(nblk, c->K), 256, 0, s>>>(params, c->d_woffs, LW, c->d_rtr, c->d_wsnap,
+                                                            c->proj_part, nblk));
   }
   RUN(c, "pack_weights", 0.0, 0.0, pack_tagged_kernel<<<dim3(c->prep_blocks, c->n_prep), 256, 0, s>>>(c->d_prep, params, nullptr));
   return DBSDE_OK;
