@@ -1967,13 +1967,22 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       // [s n32 / S, (s + 1) n32 / S), so the chunk boundary must be a slice
       // boundary).  Profiled steps keep them after the section, so the section
       // and the weight-gradient kernel are timed on their own.
-      int sb = 0;   // first slice of chunk 1
+      // sb[i]: the first slice of chunk i (sb[nch] = S); every chunk boundary
+      // must be a slice boundary that is a multiple of 8 (the kernel's
+      // slice groups)
+      std::vector<int> sb(nch + 1, 0);
       {
         const int S = c->tnw_S, n32 = Rp / 32;
-        const long long crow = (long long)cu[0] * utile * WR;
-        for (int k = 8; k < S && !sb; k += 8)
-          if (32LL * ((long long)k * n32 / S) == crow) sb = k;
-        tnw_piped = grad && c->tnw && !c->prof && nch == 2 && np == 2 && Rp % 32 == 0 && sb > 0;
+        bool ok = Rp % 32 == 0;
+        long long crow = 0;
+        sb[nch] = S;
+        for (int i = 1; i < nch && ok; ++i) {
+          crow += (long long)cu[i - 1] * utile * WR;
+          for (int k = sb[i - 1] + 8; k < S && !sb[i]; k += 8)
+            if (32LL * ((long long)k * n32 / S) == crow) sb[i] = k;
+          ok = sb[i] > 0;
+        }
+        tnw_piped = grad && c->tnw && !c->prof && np == 2 && ok;
       }
       hipStream_t ps[4] = {s, c->pipe2, c->pipe_more[0], c->pipe_more[1]};
       for (int i = 1; i < np; ++i) HIPC(c, hipStreamWaitEvent(ps[i], c->ev_pipe[0], 0));
@@ -1985,7 +1994,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         const int tiles = cu[i] * utile;
         kFused[fv].A<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         kFused[fv].C<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
-        if (tnw_piped && (rc = launch_tnw(c, R, Rp, i == 0 ? 0 : sb, i == 0 ? sb : c->tnw_S - sb, st))) return rc;
+        if (tnw_piped && (rc = launch_tnw(c, R, Rp, sb[i], sb[i + 1] - sb[i], st))) return rc;
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());

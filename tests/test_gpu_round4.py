@@ -235,14 +235,15 @@ def test_phase_chunk_count_does_not_change_the_step(pkg, dev, M):
     """The phase pipeline's path chunks (DBSDE_CHUNKS; default by occupancy:
     one chunk when a phase launch fits the chip's workgroup slots, M = 128,
     else two, M = 1024) only reorder independent rows: loss and gradient are
-    bit-identical for 1, 2 and the default."""
+    bit-identical for 1, 2, 4 (weight-gradient slices piped behind each
+    chunk) and the default."""
     g = _load("g2_north_star.npz")
     layers = [int(v) for v in g["layers"]]
     D = layers[0] - 1
     res = {}
     old = os.environ.get("DBSDE_CHUNKS")
     try:
-        for ch in ("1", "2", None):
+        for ch in ("1", "2", "4", None):
             if ch is None:
                 os.environ.pop("DBSDE_CHUNKS", None)
             else:
@@ -258,7 +259,7 @@ def test_phase_chunk_count_does_not_change_the_step(pkg, dev, M):
             os.environ.pop("DBSDE_CHUNKS", None)
         else:
             os.environ["DBSDE_CHUNKS"] = old
-    for ch in ("2", None):
+    for ch in ("2", "4", None):
         torch.testing.assert_close(res[ch][0], res["1"][0], rtol=0, atol=0)
         torch.testing.assert_close(res[ch][1], res["1"][1], rtol=0, atol=0)
 
