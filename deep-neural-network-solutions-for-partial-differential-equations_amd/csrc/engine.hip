@@ -1982,7 +1982,10 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
             if (32LL * ((long long)k * n32 / S) == crow) sb[i] = k;
           ok = sb[i] > 0;
         }
-        tnw_piped = grad && c->tnw && !c->prof && np == 2 && ok;
+        // (two chunks only: with more, a chunk's slices sit in front of the
+        // next chunk's phase A on the same stream -- 4 chunks 0.607 vs 0.495
+        // ms/step, profiles/r4_ab_chunks_piped.txt)
+        tnw_piped = grad && c->tnw && !c->prof && np == 2 && nch == 2 && ok;
       }
       hipStream_t ps[4] = {s, c->pipe2, c->pipe_more[0], c->pipe_more[1]};
       for (int i = 1; i < np; ++i) HIPC(c, hipStreamWaitEvent(ps[i], c->ev_pipe[0], 0));
