@@ -188,11 +188,8 @@ int dbsde_brownian(dbsde_ctx* ctx, const dbsde_batch* batch, float* t, float* W,
  * (the reference's next fetch_minibatch, DeepBSDE.py:247-262, drawn while the
  * current iteration runs: train() draws each iteration's batch independently
  * of the model, nd_BSPDE_case.py:371).  The rollout runs on an internal
- * stream, ordered after the work queued on the context's stream; it starts
- * once the next dbsde_loss_grad / dbsde_train_step has queued its network
- * passes (so it overlaps that step's weight-gradient tail rather than taking
- * CUs from its phase kernels), or when its batch is consumed, whichever comes
- * first (DBSDE_PF_DEFER=0 at dbsde_create: at once).  A later
+ * stream ordered after the work already queued on the context's stream, so
+ * work queued later (the current iteration) overlaps it.  A later
  * dbsde_loss_grad whose batch descriptor is identical (M, N, seed, offset,
  * path0, Xi pointer and rows; t = W = NULL) uses the prefetched paths instead
  * of rolling out; any other batch rolls out as usual.  At most two batches
