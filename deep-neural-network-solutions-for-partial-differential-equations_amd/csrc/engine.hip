@@ -83,21 +83,13 @@ struct dbsde_ctx {
   // the buffer the queued work no longer reads (dbsde_prefetch) on pf_stream
   float* xin_b[2] = {nullptr, nullptr};
   float* sdw_b[2] = {nullptr, nullptr};
-  struct Pending_t {
+  struct Pending {
     bool valid = false;
-    bool launched = false;   // deferred prefetch: rollout not enqueued yet
     dbsde_batch b{};
     hipEvent_t ready = nullptr;
     unsigned long long seq = 0;   // issue order: the older pending slot is the one replaced / reused
-  };
-  Pending_t pend[2];
+  } pend[2];
   unsigned long long pf_seq = 0;
-  // prefetched rollouts start after the next step's phase section (where
-  // the chip has room: the weight-gradient tail) instead of at once, where
-  // they take CUs from the phase kernels (bsb: 7 of the rollout's 30 us
-  // hidden, basket: the phases +70 us, profiles/r4_ab_prefetch.txt).
-  // DBSDE_PF_DEFER=0: at once.
-  bool pf_defer = true;
   hipStream_t pf_stream = nullptr;
   hipEvent_t ev_pf_order = nullptr;
   // path-chunked phase pipeline: chunk i runs phase A then phase C on stream
@@ -968,8 +960,6 @@ bool same_batch(const dbsde_batch& a, const dbsde_batch& b) {
 // batch that dbsde_prefetch already rolled out takes that buffer (the main
 // stream waits for the prefetch; from_pf = true); anything else takes a
 // buffer no pending prefetch writes.
-int launch_prefetch(dbsde_ctx* c, int j, hipStream_t after);
-
 int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
   from_pf = false;
   int use = -1;
@@ -981,60 +971,15 @@ int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
       }
   if (use < 0) {
     // a buffer no prefetch holds; both pending and neither is this batch: the
-    // older one's buffer is reused once its rollout is done (a deferred one
-    // never started: dropped)
+    // older one's buffer is reused once its rollout is done
     use = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
-    if (c->pend[use].valid && c->pend[use].launched) HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
+    if (c->pend[use].valid) HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
   } else {
-    int rc;
-    if (!c->pend[use].launched && (rc = launch_prefetch(c, use, c->stream))) return rc;
     HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
   }
   c->pend[use].valid = false;
   c->xin = c->xin_b[use];
   c->sdw = c->sdw_b[use];
-  return DBSDE_OK;
-}
-
-// enqueue pending prefetch j on the prefetch stream, after everything queued
-// so far on `after` (Xi ready, the buffer's previous readers done)
-int launch_prefetch(dbsde_ctx* c, int j, hipStream_t after) {
-  dbsde_ctx::Pending_t& pd = c->pend[j];
-  const dbsde_batch* next = &pd.b;
-  const int M = next->M, N = next->N, R = M * (N + 1), Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD;
-  HIPC(c, hipEventRecord(c->ev_pf_order, after));
-  HIPC(c, hipStreamWaitEvent(c->pf_stream, c->ev_pf_order, 0));
-  hipStream_t main_stream = c->stream;
-  float *xin0 = c->xin, *sdw0 = c->sdw;
-  c->stream = c->pf_stream;
-  c->xin = c->xin_b[j];
-  c->sdw = c->sdw_b[j];
-  int rc = DBSDE_OK;
-  (void)N;
-  hipError_t e = hipSuccess;
-  if (Rp > R) e = hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, c->stream);
-  if (e == hipSuccess) {
-    RolloutArgs ra = rollout_args(c, next);
-    ra.out = PATH_ROLLOUT;
-    rc = launch_paths(c, ra);
-  }
-  c->stream = main_stream;
-  c->xin = xin0;
-  c->sdw = sdw0;
-  if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("prefetch: ") + hipGetErrorString(e));
-  if (rc) return rc;
-  HIPC(c, hipEventRecord(pd.ready, c->pf_stream));
-  pd.launched = true;
-  return DBSDE_OK;
-}
-// the deferred prefetches not started yet, oldest first, after `after`
-int launch_deferred_prefetches(dbsde_ctx* c, hipStream_t after) {
-  const int o = c->pend[0].seq <= c->pend[1].seq ? 0 : 1;
-  for (int k = 0; k < 2; ++k) {
-    const int j = k == 0 ? o : 1 - o;
-    int rc;
-    if (c->pend[j].valid && !c->pend[j].launched && (rc = launch_prefetch(c, j, after))) return rc;
-  }
   return DBSDE_OK;
 }
 
@@ -1636,7 +1581,6 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
       rc = fail(c, DBSDE_EHIP, hipGetErrorString(e));
     if (const char* ec = getenv("DBSDE_CHUNKS")) c->chunks = std::max(0, atoi(ec));
     if (const char* ec = getenv("DBSDE_CHUNK0")) c->chunk0 = std::max(0, atoi(ec));
-    if (const char* ep = getenv("DBSDE_PF_DEFER")) c->pf_defer = ep[0] != '0';
   }
   if (!rc) rc = build_buffers(c);
   if (!rc) {
@@ -2053,9 +1997,6 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         const int tiles = cu[i] * utile;
         kFused[fv].A<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         kFused[fv].C<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
-        // the next batch's rollout after the last phase C, beside the
-        // weight-gradient tail
-        if (i == nch - 1 && !c->prof && (rc = launch_deferred_prefetches(c, st))) return rc;
         if (tnw_piped && (rc = launch_tnw(c, R, Rp, sb[i], sb[i + 1] - sb[i], st))) return rc;
         t0 += tiles;
       }
@@ -2132,7 +2073,6 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
        })))
     return rc;
 
-  if ((rc = launch_deferred_prefetches(c, s))) return rc;   // (other layouts: after the network passes)
   if (grad && (rc = backward_tail(c, params, R, Rp, fv, grad, c->loss_part, nloss_parts, loss_dst, fo, tnw_piped)))
     return rc;
 
@@ -2419,14 +2359,32 @@ int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
   // a buffer no pending prefetch holds (else the older one's is replaced: its
   // rollout is earlier on the same stream)
   const int j = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
+  // after everything queued so far on the caller's stream (Xi ready, the
+  // buffer's previous readers done); work queued later overlaps this
+  HIPC(c, hipEventRecord(c->ev_pf_order, c->stream));
+  HIPC(c, hipStreamWaitEvent(c->pf_stream, c->ev_pf_order, 0));
+  hipStream_t main_stream = c->stream;
+  float *xin0 = c->xin, *sdw0 = c->sdw;
+  c->stream = c->pf_stream;
+  c->xin = c->xin_b[j];
+  c->sdw = c->sdw_b[j];
+  hipError_t e = hipSuccess;
+  if (Rp > R) e = hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, c->stream);
+  if (e == hipSuccess) {
+    RolloutArgs ra = rollout_args(c, next);
+    ra.out = PATH_ROLLOUT;
+    rc = launch_paths(c, ra);
+  }
+  c->stream = main_stream;
+  c->xin = xin0;
+  c->sdw = sdw0;
+  if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("prefetch: ") + hipGetErrorString(e));
+  if (rc) return rc;
+  HIPC(c, hipEventRecord(c->pend[j].ready, c->pf_stream));
   c->pend[j].valid = true;
-  c->pend[j].launched = false;
   c->pend[j].b = *next;
   c->pend[j].seq = ++c->pf_seq;
-  // deferred: enqueued by the next step after its phase section, or when
-  // consumed (select_paths)
-  if (c->pf_defer) return DBSDE_OK;
-  return launch_prefetch(c, j, c->stream);
+  return DBSDE_OK;
 }
 
 int dbsde_prefetch_cancel(dbsde_ctx* c) {
