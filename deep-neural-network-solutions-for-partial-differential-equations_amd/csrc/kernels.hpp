@@ -805,12 +805,19 @@ __global__ void __launch_bounds__(256) optim_kernel(float* prm, float* g, float*
   __shared__ float clip_s;
   __shared__ int skip_s;
   __shared__ OptArgs a_s;
+  // the squared-norm partials summed by wave 0 (lane l: partials l, l + 64,
+  // ...; then a fixed xor butterfly): one thread summing 256 of them in
+  // series left every block waiting on dependent global loads
+  double ssq = 0.0;
+  if (threadIdx.x < 64 && a.max_norm > 0.f) {
+    for (int i = threadIdx.x; i < a.nparts; i += 64) ssq += part[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ssq += __shfl_xor(ssq, o);
+  }
   if (threadIdx.x == 0) {
     float coef = 1.f;
     if (a.max_norm > 0.f) {
-      double s = 0.0;
-      for (int i = 0; i < a.nparts; ++i) s += part[i];
-      const float tot = (float)sqrt(s);
+      const float tot = (float)sqrt(ssq);
       coef = a.max_norm / (tot + 1e-6f);
       if (coef > 1.f) coef = 1.f;
     }
