@@ -1300,7 +1300,8 @@ int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double*
             c->d_fin, c->n_fin, c->slabW, c->tnw_S, c->tnw_P, T, grad, loss_part, nloss, loss, f, fuse));
   } else {
     RUN(c, "grad_finalize", 0.0, 0.0,
-        slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad, c->tn_splits_cur));
+        slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad, c->tn_splits_cur, loss_part,
+                                                                      nloss, loss));
   }
   if (c->proj) {
     const int LW = c->L[1];
@@ -1860,7 +1861,7 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
   } else {
     RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
   }
-  if ((rc = finalize_grads(c, params, grad, nullptr, 0, nullptr, fo))) return rc;
+  if ((rc = finalize_grads(c, params, grad, loss_part, nloss_parts, loss_dst, fo))) return rc;
   }
   return DBSDE_OK;
 }
@@ -2064,9 +2065,9 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     nloss_parts = Rp / 256 + 1;
   }
   float* loss_dst = (out && out->loss) ? out->loss : c->loss_tmp;
-  // the loss sum: inside the gradient finalize when that is tilefin_kernel,
-  // else its own launch
-  const bool loss_in_fin = grad && c->tnw;
+  // the loss sum: inside the gradient finalize (tilefin_kernel or
+  // slabsum_kernel), else (no gradient) its own launch
+  const bool loss_in_fin = grad;
   if (!loss_in_fin && (rc = fork_side(c, 1, [&]() {
          RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, c->stream>>>(c->loss_part, nloss_parts, loss_dst));
          return DBSDE_OK;

@@ -972,7 +972,22 @@ __global__ void __launch_bounds__(1024) tn_out_kernel(const float* u16, const fl
 
 // nslab: the slabs the weight-gradient launch wrote (its row splits); a
 // descriptor's own nslab is the capacity (0: a zero window)
-__global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, float* grad, int nslab) {
+// loss (nullable): block (0, 0) also sums the loss partials into it, in
+// loss_final_kernel's fixed order (one launch fewer)
+__global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, float* grad, int nslab,
+                                                      const double* loss_part, int nloss, float* loss) {
+  if (loss && blockIdx.x == 0 && blockIdx.y == 0) {
+    __shared__ double red[256];
+    double a = 0.0;
+    for (int i = threadIdx.x; i < nloss; i += 256) a += loss_part[i];
+    red[threadIdx.x] = a;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) loss[0] = (float)red[0];
+  }
   PackDesc d = descs[blockIdx.y];
   if (d.nslab > 0) d.nslab = nslab;
   const int total = d.rows * d.cols;
