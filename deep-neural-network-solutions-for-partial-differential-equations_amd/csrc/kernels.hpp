@@ -991,58 +991,8 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
   PackDesc d = descs[blockIdx.y];
   if (d.nslab > 0) d.nslab = nslab;
   const int total = d.rows * d.cols;
-  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  // whole-row windows of 16-byte-aligned slabs: four columns per lane (float4
-  // loads, a 1 KB row piece per wave load), 256 elements per block, the same
-  // per-element summation order as the scalar form below
-  const bool vec = !d.dotR && d.cols % 4 == 0 && d.src_ld % 4 == 0 && d.slab_stride % 4 == 0 &&
-                   ((uintptr_t)d.src & 15) == 0;
-  if (vec) {
-    if ((int)blockIdx.x * 256 >= total) return;
-    const int e0 = blockIdx.x * 256 + 4 * lane;
-    double s4[4] = {0.0, 0.0, 0.0, 0.0};
-    int r = 0, cc = 0;
-    if (e0 < total) {
-      r = e0 / d.cols;
-      cc = e0 - r * d.cols;
-      const float* src = d.src + (size_t)r * d.src_ld + cc;
-      const int k0 = grp * d.nslab / 4, k1 = (grp + 1) * d.nslab / 4;
-      int k = k0;
-      for (; k + 8 <= k1; k += 8) {
-        floatx4 x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = *(const floatx4*)(src + (size_t)(k + u) * d.slab_stride);
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          s4[c] += (((double)x[0][c] + (double)x[1][c]) + ((double)x[2][c] + (double)x[3][c])) +
-                   (((double)x[4][c] + (double)x[5][c]) + ((double)x[6][c] + (double)x[7][c]));
-      }
-      for (; k < k1; ++k) {
-        const floatx4 x = *(const floatx4*)(src + (size_t)k * d.slab_stride);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) s4[c] += x[c];
-      }
-    }
-    __shared__ double part4[4][4][64];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) part4[grp][c][lane] = s4[c];
-    __syncthreads();
-    if (grp == 0 && e0 < total) {
-      uintptr_t dv = (uintptr_t)d.dst;
-      float* dst = (dv & ((uintptr_t)1 << 61)) ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float v =
-            d.scale * (float)((part4[0][c][lane] + part4[1][c][lane]) + (part4[2][c][lane] + part4[3][c][lane]));
-        if (d.transpose)
-          dst[(size_t)(cc + c) * d.dst_ld + r] = v;
-        else
-          dst[(size_t)r * d.dst_ld + cc + c] = v;
-      }
-    }
-    return;
-  }
   if ((int)blockIdx.x * 64 >= total) return;
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + lane;
   double s = 0.0;
   int r = 0, cc = 0;
