@@ -78,7 +78,10 @@ __device__ __forceinline__ void tx3_store(const TnX3Step& s, uintx4* img) {
 // eight contiguous runs of (tile, split, problem), one per XCD -- the tiles of
 // one split, which share their A / B column strips, run together on one XCD
 // and read the strips once into its L2 instead of once per tile.
-__global__ void __launch_bounds__(256, 2) tn_x3_kernel(TNArgs args, int rps) {
+#ifndef DBSDE_TNX3_WAVES
+#define DBSDE_TNX3_WAVES 2   // waves per SIMD the register budget targets
+#endif
+__global__ void __launch_bounds__(256, DBSDE_TNX3_WAVES) tn_x3_kernel(TNArgs args, int rps) {
   const int nx = gridDim.x, ny = gridDim.y;
   int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
   const int per = nx * ny * gridDim.z / 8;
