@@ -79,7 +79,7 @@ __device__ __forceinline__ void tx3_store(const TnX3Step& s, uintx4* img) {
 // one split, which share their A / B column strips, run together on one XCD
 // and read the strips once into its L2 instead of once per tile.
 #ifndef DBSDE_TNX3_WAVES
-#define DBSDE_TNX3_WAVES 2   // waves per SIMD the register budget targets
+#define DBSDE_TNX3_WAVES 3   // waves per SIMD the register budget targets (168 VGPRs; 2: 184, HJB 0.283 vs 0.267-0.271 ms)
 #endif
 __global__ void __launch_bounds__(256, DBSDE_TNX3_WAVES) tn_x3_kernel(TNArgs args, int rps) {
   const int nx = gridDim.x, ny = gridDim.y;
