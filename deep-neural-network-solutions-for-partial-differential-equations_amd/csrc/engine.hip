@@ -97,9 +97,9 @@ struct dbsde_ctx {
   hipStream_t pipe2 = nullptr;
   hipStream_t pipe_more[2] = {nullptr, nullptr};   // streams 3 and 4 (DBSDE_PIPES=3|4)
   int pipes = 2;
-  // bit i: fork_side(i) work stays on the main stream.  Default: both (the
+  // bit i: fork_side(i) work stays on the main stream.  Both (the
   // cross-stream event hops cost more than the overlap of the small prep /
-  // loss kernels gains, -12 us/step measured); DBSDE_SERIAL=0 forks them.
+  // loss kernels gains, -12 us/step measured).
   int serial = 3;
   hipEvent_t ev_pipe[2] = {nullptr, nullptr};
   hipEvent_t ev_more[2] = {nullptr, nullptr};
@@ -108,7 +108,6 @@ struct dbsde_ctx {
   // than the chip has slots (below that the chunks only serialize: A0, C0 || A1,
   // C1 is three workgroup lifetimes against A, C's two); DBSDE_CHUNKS=n forces n
   int chunks = 0;
-  int chunk0 = 0;
   int cus = 256;   // compute units of the device
   int fv_slots[64] = {0};   // resident workgroups of the chip per phase variant (lazily queried)
   int fv_cs = -1;           // the column-split variant of fv (phasecs.hpp), or -1
@@ -175,8 +174,6 @@ struct dbsde_ctx {
   float* rowsum = nullptr;        // [Rp, 8] residual row sums (fused path)
   bool fused = false;             // wave-level fused phase kernels usable for this net
   bool x3 = false;                // ... in their split-bf16 form (phase.hpp)
-  bool nt2 = false;               // ... with two 16-row tiles per wave where built (phase2.hpp; DBSDE_NT=2)
-  bool adot = false;              // ... phase C with adot in memory where both forms exist (DBSDE_ADOT=1)
   int fv = -1;                    // the fused variant (kFused index) or -1
   bool x3chain = false;           // per-layer chain GEMMs in split-bf16 form (chainx3.hpp)
   bool tnx3 = false;              // the split-K weight-gradient tiles in split-bf16 form (tnx3.hpp; !tnw layouts)
@@ -337,23 +334,18 @@ const FusedVariant kFused[] = {
 #undef FV
 constexpr int kNumFused = (int)(sizeof(kFused) / sizeof(kFused[0]));
 static_assert(kNumFused <= 64, "dbsde_ctx::fv_slots");
-// the variant for a network: rows_max 128 admits the two-tile kernels
-// (preferred when admitted), 64 only the others; adot selects between the
-// register and the memory adot form where both exist
+// the variant for a network (each (T, TD, K, act, hv, x3) has at most one
+// 64-row and one column-split instance)
 // (DBSDE_W256=0 leaves the width-256 FC networks to the per-layer chain)
 // (cs: the column-split variant, which the launch picks for small batches)
-int fused_variant(int T, int TD, int K, int act, bool hv, bool x3, int rows_max = P3_ROWS, bool adot = false,
-                  bool cs = false) {
+int fused_variant(int T, int TD, int K, int act, bool hv, bool x3, bool cs = false) {
   const char* ew = getenv("DBSDE_W256");
   const bool wide = !(ew && ew[0] == '0');
-  int any = -1;
   for (int i = 0; i < kNumFused; ++i)
-    if ((wide || kFused[i].T <= 8) && kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K && kFused[i].act == act && kFused[i].hv == hv &&
-        kFused[i].x3 == (int)x3 && kFused[i].rows <= rows_max && (kFused[i].rows == CS_ROWS) == cs) {
-      if (kFused[i].adot == (int)adot) return i;
-      if (any < 0) any = i;
-    }
-  return any;
+    if ((wide || kFused[i].T <= 8) && kFused[i].T == T && kFused[i].TD == TD && kFused[i].K == K &&
+        kFused[i].act == act && kFused[i].hv == hv && kFused[i].x3 == (int)x3 && (kFused[i].rows == CS_ROWS) == cs)
+      return i;
+  return -1;
 }
 
 // ---------------------------------------------------------------------------
@@ -453,23 +445,17 @@ int build_net(dbsde_ctx* c) {
   const bool allow = !(env && env[0] == '0');
   const char* ex3 = getenv("DBSDE_X3");
   const bool want_x3 = !(ex3 && ex3[0] == '0');
-  const char* ent = getenv("DBSDE_NT");
-  c->nt2 = ent && ent[0] == '2';
-  const char* ead = getenv("DBSDE_ADOT");
-  c->adot = ead && ead[0] == '1';
   c->x3 = want_x3 && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, true) >= 0;
   c->fused = allow && uniform && fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3) >= 0;
   c->x3 = c->x3 && c->fused;
-  c->fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3, c->nt2 ? Q_ROWS : P3_ROWS,
-                                   c->adot)
-                   : -1;
+  c->fv = c->fused ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, c->x3) : -1;
   // the column-split form for small batches (DBSDE_CS=0 never, =1 always,
   // default when the 64-row kernels would fill at most half the chip's slots)
   {
     const char* ecs = getenv("DBSDE_CS");
     c->cs_mode = !ecs ? 2 : (ecs[0] == '0' ? 0 : 1);
     c->fv_cs = (c->fv >= 0 && c->cs_mode && kFused[c->fv].rows == P3_ROWS && c->x3)
-                   ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, true, P3_ROWS, false, true)
+                   ? fused_variant(c->Wp[0] / 16, c->Dp / 16, c->K, c->act, c->has_v, true, true)
                    : -1;
   }
   // FC / Resnet layouts the fused kernels do not cover: split-bf16 chain GEMMs
@@ -882,7 +868,10 @@ void x3_weights(dbsde_ctx* c, ChainArgs& a, const float* img, int tout, int ti) 
   a.x3_ti = ti;
 }
 
-constexpr int ROW_PAD = Q_ROWS;    // rows per phase-kernel workgroup (a multiple of the chain-GEMM tile, 64)
+// rows per 64-row phase-kernel workgroup (a multiple of the chain-GEMM tile,
+// 64, and of the column-split workgroup, 16)
+constexpr int ROW_PAD = P3_ROWS;
+static_assert(ROW_PAD % CS_ROWS == 0, "row padding");
 
 RolloutArgs rollout_args(dbsde_ctx* c, const dbsde_batch* b) {
   const dbsde_problem& pr = c->cfg.problem;
@@ -1581,7 +1570,6 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     else if ((e = hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, cfg->device)) != hipSuccess)
       rc = fail(c, DBSDE_EHIP, hipGetErrorString(e));
     if (const char* ec = getenv("DBSDE_CHUNKS")) c->chunks = std::max(0, atoi(ec));
-    if (const char* ec = getenv("DBSDE_CHUNK0")) c->chunk0 = std::max(0, atoi(ec));
   }
   if (!rc) rc = build_buffers(c);
   if (!rc) {
@@ -1951,14 +1939,9 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     } else {
       // phase A / phase C of chunk i on stream (i even ? main : pipe2); the
       // two phases are timed as one pipelined segment
-      // chunk sizes in units of WR paths; DBSDE_CHUNK0 sets the first chunk's
-      // units (the rest split evenly), else all chunks are equal
+      // equal chunks in units of WR paths
       const int units = M / WR, utile = N1;   // WR paths = N1 tiles
       std::vector<int> cu(nch, units / nch);
-      if (c->chunk0 > 0 && c->chunk0 < units && nch == 2) {
-        cu[0] = c->chunk0;
-        cu[1] = units - c->chunk0;
-      }
       if (c->prof) HIPC(c, hipEventRecord(c->ev_prof[0], s));
       HIPC(c, hipEventRecord(c->ev_pipe[0], s));
       const int np = std::min(c->pipes, nch);
@@ -1995,7 +1978,11 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         hipStream_t st = ps[i % np];
         FusedArgs fc = fa;
         fc.tile0 = t0;
-        const int tiles = cu[i] * utile;
+        // the last chunk also runs the padding tiles past R (Rp > R when the
+        // workgroup is 16 rows and R is not a multiple of the 64-row padding):
+        // the loss partials and the weight-gradient rows of every tile up to
+        // Rp / WR are then written by this step
+        const int tiles = i + 1 < nch ? cu[i] * utile : Rp / WR - t0;
         kFused[fv].A<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         kFused[fv].C<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         if (tnw_piped && (rc = launch_tnw(c, R, Rp, sb[i], sb[i + 1] - sb[i], st))) return rc;

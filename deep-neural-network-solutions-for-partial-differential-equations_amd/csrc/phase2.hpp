@@ -22,9 +22,6 @@
 
 namespace dbsde {
 
-constexpr int Q_NT = 2;                            // 16-row tiles per wave (width-112 kernels)
-constexpr int Q_ROWS = 16 * Q_NT * P3_WAVES;       // rows per workgroup of those
-
 // Template parameters of the phase2 kernels:
 //   T, TD   level / state width in 16-column blocks (T != TD: runtime piece
 //           tables, pieces of 3 TO fragments for the stage's TO)

@@ -87,26 +87,35 @@ class _NetU(torch.autograd.Function):
 class _Loss(torch.autograd.Function):
     """FBSNN.loss_function's loss as a graph-connected scalar (the reference
     returns it with the graph built, DeepBSDE.py:278-279 / nd_BSPDE_case.py:378
-    call loss.backward() on it).  The forward runs dbsde_loss_grad once, which
-    yields the loss and its parameter gradient together; the backward scales
-    that gradient by the incoming cotangent and splits it into the model
-    parameters.  t, W and Xi are not differentiated."""
+    call loss.backward() on it).  The forward is the forward-only native pass
+    (dbsde_loss_grad without a gradient), so a caller that only evaluates or
+    logs the loss pays no backward; it keeps the batch and a copy of the flat
+    parameters (0.37 MB at the north star), and the backward runs
+    dbsde_loss_grad on them -- the gradient of the weights the loss was
+    evaluated at, as the reference's saved graph gives even if the parameters
+    change in between -- scales it by the incoming cotangent and splits it
+    into the model parameters.  t, W and Xi are not differentiated; X and Y
+    are returned detached (a loss built from Y gets no gradient through it:
+    INTEGRATION.md)."""
 
     @staticmethod
     def forward(ctx, fb, t, W, Xi, *params):
-        g = torch.empty_like(fb.params)
-        out = fb._run(t, W, Xi, grad=g)
+        out = fb._run(t, W, Xi)
         ctx.fb = fb
-        ctx.save_for_backward(g)
+        ctx.batch = (t, W, Xi)
+        ctx.save_for_backward(fb.params.detach().clone())
         ctx.mark_non_differentiable(out["X"], out["Y"])
         return out["loss"][0].clone(), out["X"], out["Y"]
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, gl, gX, gY):
-        (g,) = ctx.saved_tensors
         if gl is None:
             return (None,) * (4 + len(ctx.fb._param_slices()))
+        (snap,) = ctx.saved_tensors
+        t, W, Xi = ctx.batch
+        g = torch.empty_like(snap)
+        ctx.fb._run(t, W, Xi, grad=g, want=(), params=snap)
         return (None, None, None, None) + ctx.fb._param_grads(g * gl.float())
 
 
@@ -244,8 +253,9 @@ class FBSNN(ABC):
         xi = self._xi_rows(self.Xi, M)
         return xi if xi.shape[0] == 1 else xi[p0:p0 + ml].contiguous()
 
-    def _run(self, t, W, Xi, grad=None, want=("X", "Y"), loss=None):
-        """One native loss(+grad) evaluation over the paths of t/W."""
+    def _run(self, t, W, Xi, grad=None, want=("X", "Y"), loss=None, params=None):
+        """One native loss(+grad) evaluation over the paths of t/W (at the
+        model's parameters, or the flat vector `params`)."""
         M, N1 = t.shape[0], t.shape[1]
         N, Ds, nb = N1 - 1, self.state_dim, self.solver.nb
         Xi = self._xi_rows(Xi, M)
@@ -258,7 +268,7 @@ class FBSNN(ABC):
             out["Z"] = torch.empty((M, N1, Ds), device=self.device)
         t = torch.as_tensor(t, dtype=torch.float32).to(self.device)
         W = torch.as_tensor(W, dtype=torch.float32).to(self.device)
-        self.solver.loss_grad(self.params, M, N, Xi, t=t.reshape(M, N1).contiguous(),
+        self.solver.loss_grad(self.params if params is None else params, M, N, Xi, t=t.reshape(M, N1).contiguous(),
                               W=W.reshape(M, N1, nb).contiguous(), grad=grad, loss=out["loss"],
                               X=out.get("X"), Y=out.get("Y"), Z=out.get("Z"))
         return out
@@ -314,8 +324,8 @@ class FBSNN(ABC):
         """nd_BSPDE_case.py:237-281 -> (loss, X, Y, Y[0,0,0]).  With grad mode
         on and the model's parameters requiring grad, the loss is connected to
         them like the reference's: loss.backward() accumulates the native
-        gradient (dbsde_loss_grad) into each parameter's .grad.  X and Y are
-        returned detached."""
+        gradient (dbsde_loss_grad, run by the backward) into each parameter's
+        .grad.  X and Y are returned detached."""
         params = [p for _, p in self.model.named_parameters()]
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
             loss, X, Y = _Loss.apply(self, t, W, Xi, *params)

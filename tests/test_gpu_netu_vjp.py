@@ -2,8 +2,10 @@
 Du = du/dX with create_graph=True, so a loss on (u, Du) back-propagates into
 the network parameters).  The native backward is dbsde_net_u_vjp -- the
 loss_grad backward with the caller's cotangents -- on the fused split-bf16
-kernels (NAIS-Net 4x110), the fp32 fused width-16 kernels and the per-layer
-chain (FC 4x256).  Checked against the oracle's autograd (oracle/fbsnn_ref.py
+kernels (NAIS-Net 4x110), the fp32 fused width-16 kernels, the fused
+width-256 kernels (phase2.hip: FC-Sine [101,256x4,1] and [2,256x4,1], configs
+4 and 1) and the per-layer chain (FC 4x256 at D = 20, which has no fused
+instance).  Checked against the oracle's autograd (oracle/fbsnn_ref.py
 net_u, torch CPU) on the same weights, points and cotangents.  Needs a GPU."""
 import numpy as np
 import pytest
@@ -25,14 +27,20 @@ def dev():
     return torch.device("cuda:0")
 
 
-@pytest.mark.parametrize("mode,layers,act", [("NAIS-Net", [101] + 4 * [110] + [1], "Sine"),
-                                             ("Naisnet", [6] + 4 * [16] + [1], "Tanh"),
-                                             ("FC", [21] + 4 * [256] + [1], "Sine")],
-                         ids=["nais110_x3", "naisnet16", "fc256_chain"])
-def test_net_u_backward_matches_reference_autograd(pkg, dev, mode, layers, act):
+@pytest.mark.parametrize("mode,layers,act,form", [("NAIS-Net", [101] + 4 * [110] + [1], "Sine", 1),
+                                                  ("Naisnet", [6] + 4 * [16] + [1], "Tanh", None),
+                                                  ("FC", [21] + 4 * [256] + [1], "Sine", 4),
+                                                  ("FC", [101] + 4 * [256] + [1], "Sine", 1),
+                                                  ("FC", [2] + 4 * [256] + [1], "Sine", 1)],
+                         ids=["nais110_x3", "naisnet16", "fc256_chain", "fc256_fused_d100", "fc256_fused_d1"])
+def test_net_u_backward_matches_reference_autograd(pkg, dev, mode, layers, act, form):
+    """form: the solver.matrix_form bit the case must run on (1 = the fused
+    split-bf16 phase kernels, 4 = the split-bf16 per-layer chain)."""
     D = layers[0] - 1
     torch.manual_seed(0)
     m = pkg.BlackScholesBarenblatt(np.ones((1, D)), 1.0, 8, 5, D, layers, mode, act, device=dev)
+    if form is not None:
+        assert m.solver.matrix_form & form, f"expected matrix_form bit {form}, got {m.solver.matrix_form}"
     oracle = ref.build_model(mode, layers, act)
     ref.set_flat_params(oracle, m.params.cpu().numpy())
     rs = np.random.RandomState(1)

@@ -57,19 +57,18 @@ def dev():
     return torch.device("cuda:0")
 
 
-def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=1, cs=None):
+def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, cs=None):
     """fused=False forces the per-layer chain-GEMM path (DBSDE_FUSED=0 at
     create); tnw=False the split-K weight-gradient GEMM (DBSDE_TNW=0); x3=False
     the fp32-input MFMA form of the fused phase and weight-gradient kernels
-    (DBSDE_X3=0 / DBSDE_TNW_X3=0) instead of the split-bf16 one; nt=1 the
-    one-tile-per-wave phase kernels (DBSDE_NT=1) where the two-tile ones
-    (phase2.hip) exist; cs "0" / "1" never / always the column-split phase
+    (DBSDE_X3=0 / DBSDE_TNW_X3=0) instead of the split-bf16 one; cs "0" / "1"
+    never / always the column-split phase
     kernels (phasecs.hip; default: by batch size, so the small fixtures run
     them)."""
     layers = [int(v) for v in g["layers"]]
     D = layers[0] - 1
     env = {"DBSDE_FUSED": "1" if fused else "0", "DBSDE_TNW": "1" if tnw else "0",
-           "DBSDE_X3": "1" if x3 else "0", "DBSDE_TNW_X3": "1" if x3 else "0", "DBSDE_NT": str(nt)}
+           "DBSDE_X3": "1" if x3 else "0", "DBSDE_TNW_X3": "1" if x3 else "0"}
     old = {k: os.environ.get(k) for k in list(env) + ["DBSDE_CS"]}
     os.environ.pop("DBSDE_CS", None)
     if cs is not None:
@@ -86,10 +85,10 @@ def make_solver(pkg, dev, g, fused=True, tnw=True, x3=True, nt=1, cs=None):
                 os.environ[k] = v
 
 
-def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, nt=1, cs=None):
+def native_case(pkg, dev, g, want_grad=True, fused=True, x3=True, cs=None):
     layers = [int(v) for v in g["layers"]]
     D, M, N = layers[0] - 1, int(g["M"]), int(g["N"])
-    s = make_solver(pkg, dev, g, fused, x3=x3, nt=nt, cs=cs)
+    s = make_solver(pkg, dev, g, fused, x3=x3, cs=cs)
     params = torch.from_numpy(g["params"]).to(dev)
     out = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (N + 1) * D, device=dev),
                Y=torch.empty(M * (N + 1), device=dev), Z=torch.empty(M * (N + 1) * D, device=dev))
