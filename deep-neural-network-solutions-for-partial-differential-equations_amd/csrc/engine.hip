@@ -151,6 +151,7 @@ struct dbsde_ctx {
   int prep_blocks = 1;   // pack_tagged_kernel grid.x: one element per thread
   PackDesc* d_fin = nullptr;
   int n_fin = 0;
+  TileFinTable* d_fintab = nullptr;   // tilefin_kernel: d_fin's windows grouped by problem tile
   std::vector<float*> slab;  // TN problem slabs (0 = x-stack, j = block j)
   std::vector<int> slab_mt, slab_nt, slab_mv, slab_nv;
   double* opt_part = nullptr;
@@ -745,6 +746,19 @@ int build_buffers(dbsde_ctx* c) {
   c->n_fin = (int)F.size();
   c->fin_blocks = 1;
   for (const PackDesc& d : F) c->fin_blocks = std::max(c->fin_blocks, (d.rows * d.cols + 63) / 64);
+  if (c->tnw) {
+    // the windows of each problem tile (and, row P, the zero windows)
+    TileFinTable tab{};
+    const int Pn = c->tnw_P;
+    if (Pn > TNW_PMAX_FIN) return fail(c, DBSDE_EINVAL, "internal: finalize table");
+    for (const PackDesc& d : F) {
+      const int row = d.nslab != 0 ? d.sp : Pn;
+      if (row < 0 || row > Pn || tab.n[row] >= TF_WMAX) return fail(c, DBSDE_EINVAL, "internal: finalize windows");
+      tab.w[row][tab.n[row]++] = d;
+    }
+    if ((rc = dalloc_t(c, &c->d_fintab, 1))) return rc;
+    HIPC(c, hipMemcpy(c->d_fintab, &tab, sizeof(tab), hipMemcpyHostToDevice));
+  }
   if ((rc = dalloc_t(c, &c->d_prep, P.size()))) return rc;
   if ((rc = dalloc_t(c, &c->d_fin, F.size()))) return rc;
   // descriptors are stored with tagged pointers; the kernel arguments carry the
@@ -1286,7 +1300,7 @@ int finalize_grads(dbsde_ctx* c, const float* params, float* grad, const double*
     const int T = c->Dp;
     RUN(c, fuse ? "grad_finalize_update" : "grad_finalize", 0.0, 0.0,
         tilefin_kernel<<<dim3((T * T + TF_ELEMS - 1) / TF_ELEMS, c->tnw_P + 1), 256, 0, s>>>(
-            c->d_fin, c->n_fin, c->slabW, c->tnw_S, c->tnw_P, T, grad, loss_part, nloss, loss, f, fuse));
+            c->d_fintab, c->slabW, c->tnw_S, c->tnw_P, T, grad, loss_part, nloss, loss, f, fuse));
   } else {
     RUN(c, "grad_finalize", 0.0, 0.0,
         slabsum_kernel<<<dim3(c->fin_blocks, c->n_fin), 256, 0, s>>>(c->d_fin, grad, c->tn_splits_cur, loss_part,

@@ -1045,11 +1045,31 @@ __global__ void __launch_bounds__(256) slabsum_kernel(const PackDesc* descs, flo
 // descriptor window that covers it (W, biases, Abar + its <Abar, R> partial).
 // grid (ceil(T*T / 256), P + 1): y = P zero-fills the nslab == 0 windows.
 constexpr int TF_ELEMS = 256;   // elements per block (64 lanes x float4)
+constexpr int TF_WMAX = 16;     // descriptor windows per problem tile
+constexpr int TNW_PMAX_FIN = 16;   // problem tiles of the wave-owned layouts (2K + 2 <= 14)
+// The finalize's descriptor windows grouped by problem on the host (one row
+// per problem p < P, row P = the zero windows): a block loads its row with one
+// parallel copy instead of scanning every descriptor in thread 0 (a chain of
+// dependent global loads, ~17 round trips per block)
+struct TileFinTable {
+  int n[TNW_PMAX_FIN + 1];
+  PackDesc w[TNW_PMAX_FIN + 1][TF_WMAX];
+};
 #ifndef DBSDE_DEVICE_HELPERS_ONLY
-__global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int ndesc, const float* slab, int S,
-                                                      int P, int T, float* grad, const double* loss_part, int nloss,
-                                                      float* loss, FusedOpt fo, int fuse) {
+// the block's window row into LDS: every thread copies dwords in parallel
+__device__ __forceinline__ int tilefin_windows(const TileFinTable* tab, int p, PackDesc* wins) {
+  constexpr int NW = (int)(sizeof(PackDesc) * TF_WMAX / 4);
+  const unsigned* src = (const unsigned*)&tab->w[p][0];
+  unsigned* dst = (unsigned*)wins;
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) dst[i] = src[i];
+  return tab->n[p];
+}
+__global__ void __launch_bounds__(256) tilefin_kernel(const TileFinTable* tab, const float* slab, int S, int P, int T,
+                                                      float* grad, const double* loss_part, int nloss, float* loss,
+                                                      FusedOpt fo, int fuse) {
   const int p = blockIdx.y;
+  __shared__ PackDesc wins[TF_WMAX];
+  const int nwin = tilefin_windows(tab, p, wins);
   if (p == P) {   // zero windows (NAIS-Net's never-used input_layers[K])
     if (fuse) fused_opt_prologue(fo, blockIdx.x == 0);
     // and, in block 0, the loss sum (loss_final_kernel's fixed order: one
@@ -1066,9 +1086,9 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
       }
       if (threadIdx.x == 0) loss[0] = (float)red[0];
     }
-    for (int i = 0; i < ndesc; ++i) {
-      const PackDesc& d = descs[i];
-      if (d.nslab != 0) continue;
+    __syncthreads();
+    for (int i = 0; i < nwin; ++i) {
+      const PackDesc& d = wins[i];
       uintptr_t dv = (uintptr_t)d.dst;
       float* dst = (dv & ((uintptr_t)1 << 61)) ? grad + ((dv & (((uintptr_t)1 << 61) - 1)) >> 2) : d.dst;
       const int total = d.rows * d.cols;
@@ -1079,17 +1099,6 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int TT = T * T;
   const int e0 = blockIdx.x * TF_ELEMS + 4 * lane;   // T % 4 == 0: the float4 stays in one row
-  // this problem's windows, compacted into LDS once per block (the scatter
-  // below then walks 2-5 windows, not every descriptor)
-  constexpr int TF_WMAX = 16;
-  __shared__ PackDesc wins[TF_WMAX];
-  __shared__ int nwin_s;
-  if (threadIdx.x == 0) {
-    int n = 0;
-    for (int i = 0; i < ndesc && n < TF_WMAX; ++i)
-      if (descs[i].nslab != 0 && descs[i].sp == p) wins[n++] = descs[i];
-    nwin_s = n;
-  }
   const long long stride = (long long)P * TT;
   double s4[4] = {0.0, 0.0, 0.0, 0.0};
   if (e0 < TT) {
@@ -1128,7 +1137,6 @@ __global__ void __launch_bounds__(256) tilefin_kernel(const PackDesc* descs, int
   // instead of four dependent rounds in one wave
   double dp = 0.0;
   const PackDesc* dotd = nullptr;
-  const int nwin = nwin_s;
   if (e0 < TT) {
     const int r = e0 / T, c00 = e0 - r * T, c = grp;
     const double v = (part[0][c][lane] + part[1][c][lane]) + (part[2][c][lane] + part[3][c][lane]);

@@ -8,7 +8,7 @@ for i in 1 2 3 4 5 6; do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$@" > "$log" 2>&1
   rc=$?
   if [ $rc -eq 3 ] || grep -q "status=transient" "$log"; then
-    echo "transient (attempt $i), retrying" >> "$log.retries"; sleep 60; continue
+    echo "transient (attempt $i), retrying" >> "$log.retries"; sleep 200; continue
   fi
   exit $rc
 done
