@@ -75,10 +75,6 @@ struct dbsde_ctx {
   std::string err;
   hipStream_t stream = nullptr;
   int device = 0;
-  // second stream for the short launches that do not feed the next kernel
-  // (weight repack during the rollout, loss sum and grad clear during phase C)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
   // path buffers (xin, sdw) x 2: a device-mode rollout can be prefetched into
   // the buffer the queued work no longer reads (dbsde_prefetch) on pf_stream
   float* xin_b[2] = {nullptr, nullptr};
@@ -93,16 +89,14 @@ struct dbsde_ctx {
   hipStream_t pf_stream = nullptr;
   hipEvent_t ev_pf_order = nullptr;
   // path-chunked phase pipeline: chunk i runs phase A then phase C on stream
-  // pipe[i % 2], so one chunk's phase C fills the other's phase-A tail
+  // (main, pipe2)[i % 2], so one chunk's phase C fills the other's phase-A tail.
+  // The context creates only the streams it uses (pipe2, pf_stream): a process
+  // gets GPU_MAX_HW_QUEUES (4) hardware queues, and streams beyond that share
+  // one, where a stream's event wait also holds the other streams' work queued
+  // behind it (the prefetch stream shared the second chunk's queue, so the
+  // second chunk's phase A started after the prefetched rollout)
   hipStream_t pipe2 = nullptr;
-  hipStream_t pipe_more[2] = {nullptr, nullptr};   // streams 3 and 4 (DBSDE_PIPES=3|4)
-  int pipes = 2;
-  // bit i: fork_side(i) work stays on the main stream.  Both (the
-  // cross-stream event hops cost more than the overlap of the small prep /
-  // loss kernels gains, -12 us/step measured).
-  int serial = 3;
   hipEvent_t ev_pipe[2] = {nullptr, nullptr};
-  hipEvent_t ev_more[2] = {nullptr, nullptr};
   hipEvent_t ev_prof[2] = {nullptr, nullptr};
   // 0 = by size: two chunks only when one phase launch has more workgroups
   // than the chip has slots (below that the chunks only serialize: A0, C0 || A1,
@@ -273,28 +267,6 @@ int run(dbsde_ctx* c, const char* name, double flops, double bytes, F&& launch) 
     if (rc_) return rc_;                                   \
   } while (0)
 
-// Queue f() (launches on c->stream) on the side stream, ordered after all
-// work queued so far on the main stream; join_side(i) orders the main stream
-// after it.  Events are recorded on the stream a launch runs on, so the
-// profiler's per-kernel times stay correct.
-template <class F>
-int fork_side(dbsde_ctx* c, int i, F&& f) {
-  if (c->serial >> i & 1) return f();   // in-order on the main stream (DBSDE_SERIAL bit i)
-  HIPC(c, hipEventRecord(c->ev_fork[i], c->stream));
-  HIPC(c, hipStreamWaitEvent(c->side, c->ev_fork[i], 0));
-  hipStream_t main_stream = c->stream;
-  c->stream = c->side;
-  const int rc = f();
-  c->stream = main_stream;
-  if (rc) return rc;
-  HIPC(c, hipEventRecord(c->ev_join[i], c->side));
-  return DBSDE_OK;
-}
-int join_side(dbsde_ctx* c, int i) {
-  if (c->serial >> i & 1) return DBSDE_OK;
-  HIPC(c, hipStreamWaitEvent(c->stream, c->ev_join[i], 0));
-  return DBSDE_OK;
-}
 
 // ---------------------------------------------------------------------------
 // fused phase-kernel instantiations: (level tiles T, D tiles TD, blocks K)
@@ -1587,16 +1559,9 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
   }
   if (!rc) rc = build_buffers(c);
   if (!rc) {
-    hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->pipe2, hipStreamNonBlocking);
+    hipError_t e = hipStreamCreateWithFlags(&c->pipe2, hipStreamNonBlocking);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-      e = hipStreamCreateWithFlags(&c->pipe_more[i], hipStreamNonBlocking);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_more[i], hipEventDisableTiming);
-    }
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-      e = hipEventCreateWithFlags(&c->ev_fork[i], hipEventDisableTiming);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join[i], hipEventDisableTiming);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming);
+      e = hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming);
       if (e == hipSuccess) e = hipEventCreate(&c->ev_prof[i]);
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking);
@@ -1617,7 +1582,6 @@ void dbsde_destroy(dbsde_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->side) (void)hipStreamSynchronize(c->side);
   if (c->pipe2) (void)hipStreamSynchronize(c->pipe2);
   if (c->pf_stream) {
     (void)hipStreamSynchronize(c->pf_stream);
@@ -1626,17 +1590,10 @@ void dbsde_destroy(dbsde_ctx* c) {
   if (c->ev_pf_order) (void)hipEventDestroy(c->ev_pf_order);
   for (int i = 0; i < 2; ++i) {
     if (c->pend[i].ready) (void)hipEventDestroy(c->pend[i].ready);
-    if (c->ev_fork[i]) (void)hipEventDestroy(c->ev_fork[i]);
-    if (c->ev_join[i]) (void)hipEventDestroy(c->ev_join[i]);
     if (c->ev_pipe[i]) (void)hipEventDestroy(c->ev_pipe[i]);
     if (c->ev_prof[i]) (void)hipEventDestroy(c->ev_prof[i]);
   }
-  if (c->side) (void)hipStreamDestroy(c->side);
   if (c->pipe2) (void)hipStreamDestroy(c->pipe2);
-  for (int i = 0; i < 2; ++i) {
-    if (c->pipe_more[i]) (void)hipStreamDestroy(c->pipe_more[i]);
-    if (c->ev_more[i]) (void)hipEventDestroy(c->ev_more[i]);
-  }
   for (auto& r : c->pending) {
     c->ev_pool.push_back(r.e0);
     c->ev_pool.push_back(r.e1);
@@ -1904,7 +1861,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   const dbsde_problem& pr = c->cfg.problem;
 
   // weight repack (projection, norms, fragment images) overlaps the rollout
-  if ((rc = fork_side(c, 0, [&]() { return prep_weights(c, params); }))) return rc;
+  if ((rc = prep_weights(c, params))) return rc;
 
   // ---- rollout (network-independent: mu/sigma never read Y, Z), unless
   // dbsde_prefetch already produced this batch's paths
@@ -1918,7 +1875,6 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   }
   const bool q3 = pr.q3 && D == 1;
   if (q3) RUN(c, "q3_sum", 0.0, 4.0 * M * N, q3_sum_kernel<<<N, 256, 0, s>>>(c->sdw, c->Dp, M, N, c->q3S));
-  if ((rc = join_side(c, 0))) return rc;
 
   int nloss_parts;
   bool tnw_piped = false;
@@ -1958,7 +1914,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       std::vector<int> cu(nch, units / nch);
       if (c->prof) HIPC(c, hipEventRecord(c->ev_prof[0], s));
       HIPC(c, hipEventRecord(c->ev_pipe[0], s));
-      const int np = std::min(c->pipes, nch);
+      const int np = std::min(2, nch);
       // Unprofiled steps run each chunk's weight-gradient row slices on the
       // chunk's stream right after its phase C (the slices of the first chunk
       // overlap the second chunk's phases; slice s covers 32-row steps
@@ -1985,7 +1941,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         // ms/step, profiles/r4_ab_chunks_piped.txt)
         tnw_piped = grad && c->tnw && !c->prof && np == 2 && nch == 2 && ok;
       }
-      hipStream_t ps[4] = {s, c->pipe2, c->pipe_more[0], c->pipe_more[1]};
+      hipStream_t ps[2] = {s, c->pipe2};
       for (int i = 1; i < np; ++i) HIPC(c, hipStreamWaitEvent(ps[i], c->ev_pipe[0], 0));
       int t0 = 0;
       for (int i = 0; i < nch; ++i) {
@@ -2005,10 +1961,6 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       HIPC(c, hipGetLastError());
       HIPC(c, hipEventRecord(c->ev_pipe[1], c->pipe2));
       HIPC(c, hipStreamWaitEvent(s, c->ev_pipe[1], 0));
-      for (int i = 2; i < np; ++i) {
-        HIPC(c, hipEventRecord(c->ev_more[i - 2], ps[i]));
-        HIPC(c, hipStreamWaitEvent(s, c->ev_more[i - 2], 0));
-      }
       if (c->prof) {
         HIPC(c, hipEventRecord(c->ev_prof[1], s));
         HIPC(c, hipEventSynchronize(c->ev_prof[1]));
@@ -2069,11 +2021,8 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   // the loss sum: inside the gradient finalize (tilefin_kernel or
   // slabsum_kernel), else (no gradient) its own launch
   const bool loss_in_fin = grad;
-  if (!loss_in_fin && (rc = fork_side(c, 1, [&]() {
-         RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, c->stream>>>(c->loss_part, nloss_parts, loss_dst));
-         return DBSDE_OK;
-       })))
-    return rc;
+  if (!loss_in_fin)
+    RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, s>>>(c->loss_part, nloss_parts, loss_dst));
 
   if (grad && (rc = backward_tail(c, params, R, Rp, fv, grad, c->loss_part, nloss_parts, loss_dst, fo, tnw_piped)))
     return rc;
@@ -2084,7 +2033,6 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         export_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(c->xin, c->zfull, c->Dp, c->u, R, D, out->X,
                                                                   out->Y, out->Z, nullptr));
   }
-  if ((rc = join_side(c, 1))) return rc;
   return DBSDE_OK;
 }
 
