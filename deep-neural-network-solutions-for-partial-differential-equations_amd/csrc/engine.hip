@@ -979,6 +979,9 @@ __device__ __forceinline__ void pack_block(const PackDesc* descs, int di, const 
   d.dst = (float*)untag(d.dst, params, grad);
   const int total = d.rows * d.cols;
   if ((int)blockIdx.x * 256 >= total) return;
+  // the first element's source value in the round of the norm partials below
+  const int i0 = blockIdx.x * 256 + threadIdx.x;
+  const float rv0 = (d.mode == PK_NEGPROJ && i0 < total) ? d.src[(size_t)(i0 / d.cols) * d.src_ld + i0 % d.cols] : 0.f;
   // NAIS projection: |RtR|_F from rtr_params_kernel's partials (fixed order)
   __shared__ float nrm_s;
   if (d.mode == PK_NEGPROJ) {
@@ -1003,7 +1006,7 @@ __device__ __forceinline__ void pack_block(const PackDesc* descs, int di, const 
     } else if (d.mode == PK_ADD2) {
       v = d.src[(size_t)r * d.src_ld + cc] + d.src2[(size_t)r * d.src2_ld + cc];
     } else if (d.mode == PK_NEGPROJ) {
-      const float rv = d.src[(size_t)r * d.src_ld + cc];
+      const float rv = i == i0 ? rv0 : d.src[(size_t)r * d.src_ld + cc];
       const float nrm = nrm_s;
       float a = rv;
       if (nrm > 0.98f) a = ((float)0.98994949366116658 * rv) / sqrtf(nrm);
@@ -1062,11 +1065,26 @@ __device__ __forceinline__ void rtr_tile(const float* params, const long long* w
   const int nt = (L + 15) / 16;
   const int ti = tile / nt, tj = tile % nt;
   const float* W = params + woffs[j];
-  for (int e = threadIdx.x; e < 16 * L; e += 256) {
+  // every operand load in one round (a strided loop waited for each load
+  // before the next: ~7 dependent global round trips)
+  constexpr int PER = NAIS_LMAX * 16 / 256;
+  float av[PER], bv[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int e = threadIdx.x + 256 * u;
     const int k = e >> 4, q = e & 15;
     const int ra = 16 * ti + q, cb = 16 * tj + q;
-    As[q][k] = ra < L ? W[k * L + ra] : 0.f;
-    Bs[k][q] = cb < L ? W[k * L + cb] : 0.f;
+    av[u] = (k < L && ra < L) ? W[k * L + ra] : 0.f;
+    bv[u] = (k < L && cb < L) ? W[k * L + cb] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    const int k = e >> 4, q = e & 15;
+    if (k < L) {
+      As[q][k] = av[u];
+      Bs[k][q] = bv[u];
+    }
   }
   __syncthreads();
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -1133,6 +1151,12 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* const* 
     abs_[u] = ok ? Ab[k * L + cb] + Ab[cb * L + k] : 0.f;
     rs[u] = ok ? R[k * L + cb] + R[cb * L + k] : 0.f;
   }
+  // this thread's parameter / moments for the fused update, in the same round
+  const int row = ti * 16 + (threadIdx.x >> 4), col = tj * 16 + (threadIdx.x & 15);
+  const bool own = row < L && col < L;
+  const long long gi_idx = own ? woffs[j] + row * L + col : 0;
+  OptVals pv{};
+  if (fuse && own) pv = opt_load(gi_idx, fo.prm, fo.m, fo.v);
   // the optimizer scalars while the operand loads are in flight
   if (fuse) fused_opt_prologue(fo, false);
   if (threadIdx.x < 64) {   // <Abar_j, R_j> from the finalize partials, fixed-order butterfly
@@ -1164,13 +1188,11 @@ __global__ void __launch_bounds__(256) proj_backward_kernel(const float* const* 
   }
   __syncthreads();
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int row = ti * 16 + ty, col = tj * 16 + tx;
   float acc = 0.f;
   for (int k = 0; k < L; ++k) acc += As[ty][k] * Bs[k][tx];
-  if (row < L && col < L) {
-    const long long i = woffs[j] + row * L + col;
-    grad[i] = acc;
-    if (fuse) opt_update(fo.a, i, acc, fo.prm, fo.m, fo.v);
+  if (own) {
+    grad[gi_idx] = acc;
+    if (fuse) opt_apply(fo.a, gi_idx, acc, pv, fo.prm, fo.m, fo.v);
   }
 }
 }  // namespace dbsde

@@ -732,13 +732,22 @@ __device__ inline void opt_step_scalars(OptArgs& a, double t) {
   }
 }
 
-// one parameter element of the update: params / moments at index i, its
-// (clipped) gradient gi
-__device__ __forceinline__ void opt_update(const OptArgs& a, long long i, float gi, float* prm, float* m, float* v) {
+// a parameter element and its moments, loaded ahead of the update (the
+// finalize kernels issue these loads with their operand loads)
+struct OptVals {
+  float p, m, v;
+};
+__device__ __forceinline__ OptVals opt_load(long long i, const float* prm, const float* m, const float* v) {
+  return OptVals{prm[i], m ? m[i] : 0.f, v ? v[i] : 0.f};
+}
+// one parameter element of the update: params / moments at index i (their
+// values pv), its (clipped) gradient gi
+__device__ __forceinline__ void opt_apply(const OptArgs& a, long long i, float gi, OptVals pv, float* prm, float* m,
+                                          float* v) {
   // every product and sum rounded as written (torch's op-by-op formulas), and
   // the same in every kernel that inlines this (optim_kernel, the finalize)
 #pragma clang fp contract(off)
-  float p = prm[i];
+  float p = pv.p;
   switch (a.kind) {
     case OPT_SGD: {
       if (a.wd != 0.f) gi = gi + a.wd * p;
@@ -747,22 +756,22 @@ __device__ __forceinline__ void opt_update(const OptArgs& a, long long i, float 
     }
     case OPT_RMSPROP: {   // square_avg.mul_(alpha).addcmul_(g, g, 1-alpha); p.addcdiv_(g, sqrt(sa)+eps, -lr)
       if (a.wd != 0.f) gi = gi + a.wd * p;
-      const float sa = v[i] * a.alpha + a.omb2 * gi * gi;
+      const float sa = pv.v * a.alpha + a.omb2 * gi * gi;
       v[i] = sa;
       prm[i] = p + (-a.lr) * (gi / (sqrtf(sa) + a.eps));
       break;
     }
     case OPT_ADAGRAD: {   // state_sum.addcmul_(g, g, 1); p.addcdiv_(g, sqrt(ss)+eps, -clr)
       if (a.wd != 0.f) gi = gi + a.wd * p;
-      const float ss = v[i] + gi * gi;
+      const float ss = pv.v + gi * gi;
       v[i] = ss;
       prm[i] = p + (-a.step_size) * (gi / (sqrtf(ss) + a.eps));
       break;
     }
     case OPT_ADAMAX: {    // exp_avg.lerp_(g, 1-b1); exp_inf = max(exp_inf*b2, |g|+eps); p.addcdiv_(m, u, -clr)
       if (a.wd != 0.f) gi = gi + a.wd * p;
-      const float mi = m[i] + a.omb1 * (gi - m[i]);
-      const float ui = fmaxf(v[i] * a.beta2, fabsf(gi) + a.eps);
+      const float mi = pv.m + a.omb1 * (gi - pv.m);
+      const float ui = fmaxf(pv.v * a.beta2, fabsf(gi) + a.eps);
       m[i] = mi;
       v[i] = ui;
       prm[i] = p + (-a.step_size) * (mi / ui);
@@ -770,10 +779,10 @@ __device__ __forceinline__ void opt_update(const OptArgs& a, long long i, float 
     }
     case OPT_ADADELTA: {  // sq.mul_(rho).addcmul_(g,g,1-rho); d = sqrt(acc+eps)/sqrt(sq+eps)*g; acc.mul_(rho).addcmul_(d,d,1-rho)
       if (a.wd != 0.f) gi = gi + a.wd * p;
-      const float sq = v[i] * a.rho + a.omb2 * gi * gi;
-      const float dl = sqrtf(m[i] + a.eps) / sqrtf(sq + a.eps) * gi;
+      const float sq = pv.v * a.rho + a.omb2 * gi * gi;
+      const float dl = sqrtf(pv.m + a.eps) / sqrtf(sq + a.eps) * gi;
       v[i] = sq;
-      m[i] = m[i] * a.rho + a.omb2 * dl * dl;
+      m[i] = pv.m * a.rho + a.omb2 * dl * dl;
       prm[i] = p + (-a.lr) * dl;
       break;
     }
@@ -782,21 +791,25 @@ __device__ __forceinline__ void opt_update(const OptArgs& a, long long i, float 
       p = p * a.asgd_decay;
       p = p + (-a.asgd_eta) * gi;
       prm[i] = p;
-      m[i] = a.asgd_copy ? p : m[i] + (p - m[i]) * a.asgd_mu;
+      m[i] = a.asgd_copy ? p : pv.m + (p - pv.m) * a.asgd_mu;
       break;
     }
     default: {            // Adam / AdamW
       if (a.kind == OPT_ADAMW) p = p * (1.f - a.lr * a.wd);   // decoupled decay
       else if (a.wd != 0.f) gi = gi + a.wd * p;                // Adam L2
-      float mi = m[i];
+      float mi = pv.m;
       mi = mi + a.omb1 * (gi - mi);                            // exp_avg.lerp_(g, 1-beta1)
-      float vi = v[i] * a.beta2 + a.omb2 * gi * gi;            // mul_(beta2).addcmul_(g, g, 1-beta2)
+      float vi = pv.v * a.beta2 + a.omb2 * gi * gi;            // mul_(beta2).addcmul_(g, g, 1-beta2)
       m[i] = mi;
       v[i] = vi;
       const float denom = sqrtf(vi) / a.bc2_sqrt + a.eps;
       prm[i] = p - a.step_size * (mi / denom);                 // addcdiv_(m, denom, -step_size)
     }
   }
+}
+
+__device__ __forceinline__ void opt_update(const OptArgs& a, long long i, float gi, float* prm, float* m, float* v) {
+  opt_apply(a, i, gi, opt_load(i, prm, m, v), prm, m, v);
 }
 
 #ifndef DBSDE_DEVICE_HELPERS_ONLY
