@@ -22,6 +22,17 @@
 #include <vector>
 
 #include "../../include/dbsde.h"
+
+// the events that order the context's streams need no system-scope fence
+// (device work only; kernels carry their own device-scope release / acquire):
+// 0.4625 vs 0.4663 ms/step, M = 128 0.1448 vs 0.1474 (profiles/r5_ab_streams.txt)
+#ifndef DBSDE_EVF
+#define DBSDE_EVF (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
+// chunk fork / join through stream memory operations (stream_order)
+#ifndef DBSDE_MEMOPS
+#define DBSDE_MEMOPS 1
+#endif
 #include "kernels.hpp"
 #include "paths.hpp"
 #include "phase.hpp"
@@ -97,6 +108,14 @@ struct dbsde_ctx {
   // second chunk's phase A started after the prefetched rollout)
   hipStream_t pipe2 = nullptr;
   hipEvent_t ev_pipe[2] = {nullptr, nullptr};
+  // the fork / join of the two chunk streams as stream memory operations
+  // (a value written by one stream, waited for by the other) instead of
+  // events, when the device supports them: per step 36 us less queue time in
+  // the stream model of tools/ubench/stream_gaps.hip (events 467, no-fence
+  // events 458, value write / wait 431 us per step)
+  bool memops = false;
+  unsigned long long* d_order = nullptr;   // [slot] = last epoch written
+  unsigned long long order_epoch[2] = {0ull, 0ull};
   hipEvent_t ev_prof[2] = {nullptr, nullptr};
   // 0 = by size: two chunks only when one phase launch has more workgroups
   // than the chip has slots (below that the chunks only serialize: A0, C0 || A1,
@@ -220,6 +239,21 @@ int dalloc(dbsde_ctx* c, void** p, size_t bytes) {
 template <typename T>
 int dalloc_t(dbsde_ctx* c, T** p, size_t n) {
   return dalloc(c, (void**)p, n * sizeof(T));
+}
+
+// `to` waits until `from` has reached this point of its queue (slot 0: the
+// chunk fork, slot 1: the join).  The write is enqueued before the wait, so
+// a wait never lacks its write.
+int stream_order(dbsde_ctx* c, hipStream_t from, hipStream_t to, int slot) {
+  if (c->memops) {
+    const unsigned long long v = ++c->order_epoch[slot];
+    HIPC(c, hipStreamWriteValue64(from, c->d_order + slot, v, 0));
+    HIPC(c, hipStreamWaitValue64(to, c->d_order + slot, v, hipStreamWaitValueGte, ~0ull));
+  } else {
+    HIPC(c, hipEventRecord(c->ev_pipe[slot], from));
+    HIPC(c, hipStreamWaitEvent(to, c->ev_pipe[slot], 0));
+  }
+  return DBSDE_OK;
 }
 
 hipEvent_t get_event(dbsde_ctx* c) {
@@ -1583,13 +1617,17 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
   if (!rc) {
     hipError_t e = hipStreamCreateWithFlags(&c->pipe2, hipStreamNonBlocking);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) {
-      e = hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming);
+      e = hipEventCreateWithFlags(&c->ev_pipe[i], DBSDE_EVF);
       if (e == hipSuccess) e = hipEventCreate(&c->ev_prof[i]);
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pf_order, hipEventDisableTiming);
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pend[i].ready, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pf_order, DBSDE_EVF);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pend[i].ready, DBSDE_EVF);
     if (e != hipSuccess) rc = fail(c, DBSDE_EHIP, std::string("side stream: ") + hipGetErrorString(e));
+    int wv = 0;
+    if (!rc && DBSDE_MEMOPS && hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess &&
+        wv)
+      c->memops = (rc = dalloc_t(c, &c->d_order, 2)) == DBSDE_OK;
   }
   if (rc) {
     g_last_error = c->err;
@@ -1935,7 +1973,6 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       const int units = M / WR, utile = N1;   // WR paths = N1 tiles
       std::vector<int> cu(nch, units / nch);
       if (c->prof) HIPC(c, hipEventRecord(c->ev_prof[0], s));
-      HIPC(c, hipEventRecord(c->ev_pipe[0], s));
       const int np = std::min(2, nch);
       // Unprofiled steps run each chunk's weight-gradient row slices on the
       // chunk's stream right after its phase C (the slices of the first chunk
@@ -1964,7 +2001,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         tnw_piped = grad && c->tnw && !c->prof && np == 2 && nch == 2 && ok;
       }
       hipStream_t ps[2] = {s, c->pipe2};
-      for (int i = 1; i < np; ++i) HIPC(c, hipStreamWaitEvent(ps[i], c->ev_pipe[0], 0));
+      if (np > 1 && (rc = stream_order(c, s, c->pipe2, 0))) return rc;
       int t0 = 0;
       for (int i = 0; i < nch; ++i) {
         hipStream_t st = ps[i % np];
@@ -1981,8 +2018,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());
-      HIPC(c, hipEventRecord(c->ev_pipe[1], c->pipe2));
-      HIPC(c, hipStreamWaitEvent(s, c->ev_pipe[1], 0));
+      if ((rc = stream_order(c, c->pipe2, s, 1))) return rc;
       if (c->prof) {
         HIPC(c, hipEventRecord(c->ev_prof[1], s));
         HIPC(c, hipEventSynchronize(c->ev_prof[1]));
