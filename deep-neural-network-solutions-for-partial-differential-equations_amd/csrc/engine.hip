@@ -94,6 +94,7 @@ struct dbsde_ctx {
     bool valid = false;
     dbsde_batch b{};
     hipEvent_t ready = nullptr;
+    unsigned long long ready_v = 0;   // its order_mark token
     unsigned long long seq = 0;   // issue order: the older pending slot is the one replaced / reused
   } pend[2];
   unsigned long long pf_seq = 0;
@@ -114,8 +115,8 @@ struct dbsde_ctx {
   // the stream model of tools/ubench/stream_gaps.hip (events 467, no-fence
   // events 458, value write / wait 431 us per step)
   bool memops = false;
-  unsigned long long* d_order = nullptr;   // [slot] = last epoch written
-  unsigned long long order_epoch[2] = {0ull, 0ull};
+  unsigned long long* d_order = nullptr;   // [slot] = last epoch written (ORD_* slots)
+  unsigned long long order_epoch[8] = {};
   hipEvent_t ev_prof[2] = {nullptr, nullptr};
   // 0 = by size: two chunks only when one phase launch has more workgroups
   // than the chip has slots (below that the chunks only serialize: A0, C0 || A1,
@@ -241,19 +242,44 @@ int dalloc_t(dbsde_ctx* c, T** p, size_t n) {
   return dalloc(c, (void**)p, n * sizeof(T));
 }
 
-// `to` waits until `from` has reached this point of its queue (slot 0: the
-// chunk fork, slot 1: the join).  The write is enqueued before the wait, so
-// a wait never lacks its write.
-int stream_order(dbsde_ctx* c, hipStream_t from, hipStream_t to, int slot) {
+// Cross-stream order points: order_mark(slot, from) marks `from`'s current
+// queue position and returns its token; order_wait(slot, token, to) holds
+// `to` until `from` has passed that mark.  A wait takes the token of a mark
+// already enqueued, so it never lacks its write.  Slots: the chunk fork and
+// join, the prefetch stream after the caller's stream and back, the two
+// prefetch buffers' rollouts.
+enum { ORD_FORK = 0, ORD_JOIN = 1, ORD_PF_AFTER_MAIN = 2, ORD_MAIN_AFTER_PF = 3, ORD_PEND0 = 4 };
+hipEvent_t order_event(dbsde_ctx* c, int slot) {
+  switch (slot) {
+    case ORD_FORK: return c->ev_pipe[0];
+    case ORD_JOIN: return c->ev_pipe[1];
+    case ORD_PF_AFTER_MAIN:
+    case ORD_MAIN_AFTER_PF: return c->ev_pf_order;
+    default: return c->pend[slot - ORD_PEND0].ready;
+  }
+}
+int order_mark(dbsde_ctx* c, int slot, hipStream_t from, unsigned long long& token) {
   if (c->memops) {
-    const unsigned long long v = ++c->order_epoch[slot];
-    HIPC(c, hipStreamWriteValue64(from, c->d_order + slot, v, 0));
-    HIPC(c, hipStreamWaitValue64(to, c->d_order + slot, v, hipStreamWaitValueGte, ~0ull));
+    token = ++c->order_epoch[slot];
+    HIPC(c, hipStreamWriteValue64(from, c->d_order + slot, token, 0));
   } else {
-    HIPC(c, hipEventRecord(c->ev_pipe[slot], from));
-    HIPC(c, hipStreamWaitEvent(to, c->ev_pipe[slot], 0));
+    token = 0;
+    HIPC(c, hipEventRecord(order_event(c, slot), from));
   }
   return DBSDE_OK;
+}
+int order_wait(dbsde_ctx* c, int slot, unsigned long long token, hipStream_t to) {
+  if (c->memops)
+    HIPC(c, hipStreamWaitValue64(to, c->d_order + slot, token, hipStreamWaitValueGte, ~0ull));
+  else
+    HIPC(c, hipStreamWaitEvent(to, order_event(c, slot), 0));
+  return DBSDE_OK;
+}
+// `to` waits until `from` has reached this point of its queue
+int stream_order(dbsde_ctx* c, hipStream_t from, hipStream_t to, int slot) {
+  unsigned long long v = 0;
+  int rc = order_mark(c, slot, from, v);
+  return rc ? rc : order_wait(c, slot, v, to);
 }
 
 hipEvent_t get_event(dbsde_ctx* c) {
@@ -982,9 +1008,13 @@ int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
     // a buffer no prefetch holds; both pending and neither is this batch: the
     // older one's buffer is reused once its rollout is done
     use = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
-    if (c->pend[use].valid) HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
+    if (c->pend[use].valid) {
+      const int rc = order_wait(c, ORD_PEND0 + use, c->pend[use].ready_v, c->stream);
+      if (rc) return rc;
+    }
   } else {
-    HIPC(c, hipStreamWaitEvent(c->stream, c->pend[use].ready, 0));
+    const int rc = order_wait(c, ORD_PEND0 + use, c->pend[use].ready_v, c->stream);
+    if (rc) return rc;
   }
   c->pend[use].valid = false;
   c->xin = c->xin_b[use];
@@ -1627,7 +1657,7 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     int wv = 0;
     if (!rc && DBSDE_MEMOPS && hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess &&
         wv)
-      c->memops = (rc = dalloc_t(c, &c->d_order, 2)) == DBSDE_OK;
+      c->memops = (rc = dalloc_t(c, &c->d_order, 8)) == DBSDE_OK;
   }
   if (rc) {
     g_last_error = c->err;
@@ -2001,7 +2031,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         tnw_piped = grad && c->tnw && !c->prof && np == 2 && nch == 2 && ok;
       }
       hipStream_t ps[2] = {s, c->pipe2};
-      if (np > 1 && (rc = stream_order(c, s, c->pipe2, 0))) return rc;
+      if (np > 1 && (rc = stream_order(c, s, c->pipe2, ORD_FORK))) return rc;
       int t0 = 0;
       for (int i = 0; i < nch; ++i) {
         hipStream_t st = ps[i % np];
@@ -2018,7 +2048,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());
-      if ((rc = stream_order(c, c->pipe2, s, 1))) return rc;
+      if ((rc = stream_order(c, c->pipe2, s, ORD_JOIN))) return rc;
       if (c->prof) {
         HIPC(c, hipEventRecord(c->ev_prof[1], s));
         HIPC(c, hipEventSynchronize(c->ev_prof[1]));
@@ -2369,8 +2399,7 @@ int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
   const int j = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
   // after everything queued so far on the caller's stream (Xi ready, the
   // buffer's previous readers done); work queued later overlaps this
-  HIPC(c, hipEventRecord(c->ev_pf_order, c->stream));
-  HIPC(c, hipStreamWaitEvent(c->pf_stream, c->ev_pf_order, 0));
+  if ((rc = stream_order(c, c->stream, c->pf_stream, ORD_PF_AFTER_MAIN))) return rc;
   hipStream_t main_stream = c->stream;
   float *xin0 = c->xin, *sdw0 = c->sdw;
   c->stream = c->pf_stream;
@@ -2388,7 +2417,7 @@ int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
   c->sdw = sdw0;
   if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("prefetch: ") + hipGetErrorString(e));
   if (rc) return rc;
-  HIPC(c, hipEventRecord(c->pend[j].ready, c->pf_stream));
+  if ((rc = order_mark(c, ORD_PEND0 + j, c->pf_stream, c->pend[j].ready_v))) return rc;
   c->pend[j].valid = true;
   c->pend[j].b = *next;
   c->pend[j].seq = ++c->pf_seq;
@@ -2402,8 +2431,8 @@ int dbsde_prefetch_cancel(dbsde_ctx* c) {
   // matched any more (and are not rewritten before they are done: the stream
   // that reuses a buffer waits for the prefetch stream)
   if (c->pf_stream) {
-    HIPC(c, hipEventRecord(c->ev_pf_order, c->pf_stream));
-    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_pf_order, 0));
+    const int rc = stream_order(c, c->pf_stream, c->stream, ORD_MAIN_AFTER_PF);
+    if (rc) return rc;
   }
   c->pend[0].valid = c->pend[1].valid = false;
   return DBSDE_OK;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# prefetch ordering through stream value ops too (base) vs fork/join only (fjonly): bitwise, GPU suite, A/B, timeline
+export TMPDIR=/tmp
+out=gpurun_out/r5ab11
+mkdir -p $out
+PKG=$PWD/deep-neural-network-solutions-for-partial-differential-equations_amd
+timeout -k 10 120 python tools/grad_dump.py $out/base.npy 1024 || exit 1
+DBSDE_LIB=$PKG/lib/exp/fjonly/libdbsde.so timeout -k 10 120 python tools/grad_dump.py $out/fj.npy 1024 || exit 1
+python -c "import numpy as np; a=np.load('$out/base.npy'); b=np.load('$out/fj.npy'); print('bitwise equal:', np.array_equal(a,b))"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $out/gpu_tests.txt 2>&1; rc=$?
+tail -2 $out/gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
+bash tools/ab_libs.sh "--no-cpu-baseline --no-parity --steps 100 --warmup 50" fjonly || exit 1
+bash tools/ab_libs.sh "--no-cpu-baseline --no-parity --steps 100 --warmup 50 --paths-per-gpu 128" fjonly || exit 1
+bash tools/r5_tr.sh mo "DBSDE_X=1" --steps 60 --warmup 40 || exit 1
