@@ -19,6 +19,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <strings.h>
 #include <vector>
 
 #include "../../include/dbsde.h"
@@ -240,6 +241,22 @@ int dalloc(dbsde_ctx* c, void** p, size_t bytes) {
 template <typename T>
 int dalloc_t(dbsde_ctx* c, T** p, size_t n) {
   return dalloc(c, (void**)p, n * sizeof(T));
+}
+
+// A value wait is a kernel that spins until the value arrives, so it needs
+// the writer's queue to make progress beside it: anything that runs one kernel
+// at a time (kernel serialisation, launch blocking, rocprofv3 counter
+// collection) would never run the write.  Those environments, and
+// DBSDE_STREAM_ORDER=events, order the streams with events instead.
+bool env_set(const char* n) {
+  const char* v = getenv(n);
+  return v && v[0] && strcmp(v, "0") != 0 && strcasecmp(v, "false") != 0;
+}
+bool order_by_events() {
+  if (const char* v = getenv("DBSDE_STREAM_ORDER"))
+    if (strcmp(v, "events") == 0) return true;
+  return env_set("AMD_SERIALIZE_KERNEL") || env_set("HIP_LAUNCH_BLOCKING") || env_set("ROCPROF_COUNTER_COLLECTION") ||
+         env_set("ROCPROF_COUNTERS");
 }
 
 // Cross-stream order points: order_mark(slot, from) marks `from`'s current
@@ -1655,8 +1672,8 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pend[i].ready, DBSDE_EVF);
     if (e != hipSuccess) rc = fail(c, DBSDE_EHIP, std::string("side stream: ") + hipGetErrorString(e));
     int wv = 0;
-    if (!rc && DBSDE_MEMOPS && hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess &&
-        wv)
+    if (!rc && DBSDE_MEMOPS && !order_by_events() &&
+        hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess && wv)
       c->memops = (rc = dalloc_t(c, &c->d_order, 8)) == DBSDE_OK;
   }
   if (rc) {

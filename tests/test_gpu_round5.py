@@ -5,7 +5,9 @@
     padding (M = 96, N = 50: R = 4896, Rp = 4928): the last chunk runs the
     padding tiles, so a context that ran a larger batch before gives the
     fresh one-chunk step bit for bit (no stale loss partial or weight-gradient
-    row of the earlier batch is summed)."""
+    row of the earlier batch is summed);
+  * the streams ordered by value write / wait or by events give the same
+    training steps."""
 import os
 
 import numpy as np
@@ -67,3 +69,21 @@ def test_chunked_column_split_step_with_row_padding(pkg, dev):
     assert torch.isfinite(l1).all() and float(l1) > 0.0
     torch.testing.assert_close(l2, l1, rtol=0, atol=0)
     torch.testing.assert_close(g2, g1, rtol=0, atol=0)
+
+
+def test_stream_order_by_events_matches_value_ops(pkg, dev):
+    """The chunk fork / join and the prefetch order as stream value write /
+    wait (default) or as events (DBSDE_STREAM_ORDER=events, the fallback under
+    kernel serialisation and counter collection): four prefetched training
+    steps end on the same parameters bit for bit."""
+    g = _load("g2_north_star.npz")
+    runs = []
+    for env in ({}, {"DBSDE_STREAM_ORDER": "events"}):
+        m = _model(pkg, dev, g, env)
+        opt = m.new_optimizer_state("Adam", 1e-3)
+        for it in range(4):
+            m.device_step(opt, 1e-3, seed=11 + it, next_seed=12 + it)
+        torch.cuda.synchronize()
+        runs.append(m.params.detach().cpu().clone())
+    assert torch.isfinite(runs[0]).all()
+    torch.testing.assert_close(runs[0], runs[1], rtol=0, atol=0)
