@@ -1917,7 +1917,9 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
     for (int j = 0; j <= K; ++j)
       maxt3 = std::max(maxt3, ((ta.prob[j].nA[0] + TX_TILE - 1) / TX_TILE) * ((ta.prob[j].nB[0] + TX_TILE - 1) / TX_TILE));
     const int rps32 = ((Rp + S_ - 1) / S_ + 31) / 32 * 32;
-    if (Rp % 32 != 0 || c->Wp[K] % 4 != 0) return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
+    // tn_out_kernel's float4 loads at H + col[K] + r S: 16-byte aligned rows and column
+    if (Rp % 32 != 0 || c->Wp[K] % 4 != 0 || c->col[K] % 4 != 0 || S % 4 != 0)
+      return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
     const TNProb& po = ta.prob[K + 1];
     const long long sstride = (long long)po.mt * 64 * po.nt * 64;
     RUN(c, "tn_weight_grad", tfl, 0.0,
