@@ -96,6 +96,9 @@ struct dbsde_ctx {
     dbsde_batch b{};
     hipEvent_t ready = nullptr;
     unsigned long long ready_v = 0;   // its order_mark token
+    // the caller's stream is already ordered after this rollout (the second
+    // chunk stream waited for it before the join), so its consumer need not wait
+    bool joined = false;
     unsigned long long seq = 0;   // issue order: the older pending slot is the one replaced / reused
   } pend[2];
   unsigned long long pf_seq = 0;
@@ -1025,11 +1028,11 @@ int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
     // a buffer no prefetch holds; both pending and neither is this batch: the
     // older one's buffer is reused once its rollout is done
     use = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
-    if (c->pend[use].valid) {
+    if (c->pend[use].valid && !c->pend[use].joined) {
       const int rc = order_wait(c, ORD_PEND0 + use, c->pend[use].ready_v, c->stream);
       if (rc) return rc;
     }
-  } else {
+  } else if (!c->pend[use].joined) {
     const int rc = order_wait(c, ORD_PEND0 + use, c->pend[use].ready_v, c->stream);
     if (rc) return rc;
   }
@@ -2067,6 +2070,15 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());
+      // the pending prefetched rollouts (the next step's paths, started a step
+      // ago) are waited for on the second chunk stream, which finishes ahead of
+      // the main one, so the join orders the main stream after them too and
+      // the next step's phase A needs no wait of its own
+      for (int i = 0; i < 2; ++i)
+        if (c->pend[i].valid && !c->pend[i].joined) {
+          if ((rc = order_wait(c, ORD_PEND0 + i, c->pend[i].ready_v, c->pipe2))) return rc;
+          c->pend[i].joined = true;
+        }
       if ((rc = stream_order(c, c->pipe2, s, ORD_JOIN))) return rc;
       if (c->prof) {
         HIPC(c, hipEventRecord(c->ev_prof[1], s));
@@ -2438,6 +2450,7 @@ int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
   if (rc) return rc;
   if ((rc = order_mark(c, ORD_PEND0 + j, c->pf_stream, c->pend[j].ready_v))) return rc;
   c->pend[j].valid = true;
+  c->pend[j].joined = false;
   c->pend[j].b = *next;
   c->pend[j].seq = ++c->pf_seq;
   return DBSDE_OK;
