@@ -30,6 +30,10 @@
 #ifndef DBSDE_EVF
 #define DBSDE_EVF (hipEventDisableTiming | hipEventDisableSystemFence)
 #endif
+// a prefetched diagonal rollout runs on the next chunked step's second stream
+#ifndef DBSDE_DEFER_PF
+#define DBSDE_DEFER_PF 1
+#endif
 // chunk fork / join through stream memory operations (stream_order)
 #ifndef DBSDE_MEMOPS
 #define DBSDE_MEMOPS 1
@@ -102,6 +106,11 @@ struct dbsde_ctx {
     unsigned long long seq = 0;   // issue order: the older pending slot is the one replaced / reused
   } pend[2];
   unsigned long long pf_seq = 0;
+  // a prefetch held back for the next chunked step, which runs the rollout on
+  // its second stream after that stream's weight-gradient slices (the stream
+  // finishes ahead of the main one); other steps issue it on pf_stream
+  bool deferred = false;
+  dbsde_batch defer_b{};
   hipStream_t pf_stream = nullptr;
   hipEvent_t ev_pf_order = nullptr;
   // path-chunked phase pipeline: chunk i runs phase A then phase C on stream
@@ -1011,6 +1020,88 @@ bool same_batch(const dbsde_batch& a, const dbsde_batch& b) {
   return a.M == b.M && a.N == b.N && a.t == b.t && a.W == b.W && a.seed == b.seed && a.offset == b.offset &&
          a.path0 == b.path0 && a.Xi == b.Xi && a.xi_rows == b.xi_rows;
 }
+// dbsde_prefetch's rollout on pf_stream, ordered after everything queued so
+// far on the caller's stream
+int issue_prefetch(dbsde_ctx* c, const dbsde_batch* next, const float* avoid = nullptr) {
+  int rc;
+  const int M = next->M, N = next->N, R = M * (N + 1), Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD;
+  // a buffer no pending prefetch holds (else the older one's is replaced: its
+  // rollout is earlier on the same stream), never `avoid`
+  int j = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
+  if (c->xin_b[j] == avoid) j = 1 - j;
+  // after everything queued so far on the caller's stream (Xi ready, the
+  // buffer's previous readers done); work queued later overlaps this
+  if ((rc = stream_order(c, c->stream, c->pf_stream, ORD_PF_AFTER_MAIN))) return rc;
+  hipStream_t main_stream = c->stream;
+  float *xin0 = c->xin, *sdw0 = c->sdw;
+  c->stream = c->pf_stream;
+  c->xin = c->xin_b[j];
+  c->sdw = c->sdw_b[j];
+  hipError_t e = hipSuccess;
+  if (Rp > R) e = hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, c->stream);
+  if (e == hipSuccess) {
+    RolloutArgs ra = rollout_args(c, next);
+    ra.out = PATH_ROLLOUT;
+    rc = launch_paths(c, ra);
+  }
+  c->stream = main_stream;
+  c->xin = xin0;
+  c->sdw = sdw0;
+  if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("prefetch: ") + hipGetErrorString(e));
+  if (rc) return rc;
+  if ((rc = order_mark(c, ORD_PEND0 + j, c->pf_stream, c->pend[j].ready_v))) return rc;
+  c->pend[j].valid = true;
+  c->pend[j].joined = false;
+  c->pend[j].b = *next;
+  c->pend[j].seq = ++c->pf_seq;
+  return DBSDE_OK;
+}
+// issue a held-back prefetch on pf_stream now; avoid = the path buffer of a
+// step whose kernels are already queued (mid-step), which it must not overwrite
+int flush_deferred(dbsde_ctx* c, const float* avoid = nullptr) {
+  if (!c->deferred) return DBSDE_OK;
+  c->deferred = false;
+  const dbsde_batch b = c->defer_b;
+  return issue_prefetch(c, &b, avoid);
+}
+// the held-back prefetch on stream st (the chunked step's second stream, after
+// its weight-gradient slices), into the path buffer the current step does not
+// use; its pending entry is joined (the join write follows on st).  Falls back
+// to pf_stream when no buffer is free.
+int launch_deferred_on(dbsde_ctx* c, hipStream_t st) {
+  if (!c->deferred) return DBSDE_OK;
+  int j = -1;
+  for (int i = 0; i < 2 && j < 0; ++i)
+    if (c->xin_b[i] != c->xin && !c->pend[i].valid) j = i;
+  if (j < 0) return flush_deferred(c);
+  c->deferred = false;
+  const dbsde_batch nb = c->defer_b;
+  const int R = nb.M * (nb.N + 1), Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD;
+  hipStream_t main_stream = c->stream;
+  float *xin0 = c->xin, *sdw0 = c->sdw;
+  c->stream = st;
+  c->xin = c->xin_b[j];
+  c->sdw = c->sdw_b[j];
+  hipError_t e = hipSuccess;
+  int rc = DBSDE_OK;
+  if (Rp > R) e = hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, st);
+  if (e == hipSuccess) {
+    RolloutArgs ra = rollout_args(c, &nb);
+    ra.out = PATH_ROLLOUT;
+    rc = launch_paths(c, ra);
+  }
+  c->stream = main_stream;
+  c->xin = xin0;
+  c->sdw = sdw0;
+  if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("prefetch: ") + hipGetErrorString(e));
+  if (rc) return rc;
+  c->pend[j].valid = true;
+  c->pend[j].joined = true;
+  c->pend[j].b = nb;
+  c->pend[j].seq = ++c->pf_seq;
+  return DBSDE_OK;
+}
+
 // Point c->xin / c->sdw at the path buffer this call uses.  A device-mode
 // batch that dbsde_prefetch already rolled out takes that buffer (the main
 // stream waits for the prefetch; from_pf = true); anything else takes a
@@ -1972,6 +2063,8 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   const auto& L = c->L;
   const dbsde_problem& pr = c->cfg.problem;
 
+  // a held-back prefetch of this very batch: issue it now (its consumer)
+  if (c->deferred && same_batch(c->defer_b, *b) && (rc = flush_deferred(c))) return rc;
   // weight repack (projection, norms, fragment images) overlaps the rollout
   if ((rc = prep_weights(c, params))) return rc;
 
@@ -2017,6 +2110,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
     int nch = !grad ? 1 : (c->chunks > 0 ? c->chunks : (Rp / WR > slots ? 2 : 1));
     while (nch > 1 && (M % WR != 0 || (M / WR) % nch != 0)) --nch;
     if (nch <= 1) {
+      if ((rc = flush_deferred(c, c->xin))) return rc;
       RUN(c, "fused_fwd_inputgrad", flA, byA, kFused[fv].A<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));
     } else {
       // phase A / phase C of chunk i on stream (i even ? main : pipe2); the
@@ -2052,6 +2146,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         // ms/step, profiles/r4_ab_chunks_piped.txt)
         tnw_piped = grad && c->tnw && !c->prof && np == 2 && nch == 2 && ok;
       }
+      if (!tnw_piped && (rc = flush_deferred(c, c->xin))) return rc;
       hipStream_t ps[2] = {s, c->pipe2};
       if (np > 1 && (rc = stream_order(c, s, c->pipe2, ORD_FORK))) return rc;
       int t0 = 0;
@@ -2070,6 +2165,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());
+      if (tnw_piped && (rc = launch_deferred_on(c, c->pipe2))) return rc;
       // the pending prefetched rollouts (the next step's paths, started a step
       // ago) are waited for on the second chunk stream, which finishes ahead of
       // the main one, so the join orders the main stream after them too and
@@ -2102,6 +2198,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       nloss_parts = Rp / 16;
     }
   } else {
+    if ((rc = flush_deferred(c, c->xin))) return rc;
     if ((rc = forward_and_inputgrad(c, R, Rp, false))) return rc;
 
     // ---- Z GEMM + residuals / cotangents / loss rows
@@ -2145,6 +2242,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
 
   if (grad && (rc = backward_tail(c, params, R, Rp, fv, grad, c->loss_part, nloss_parts, loss_dst, fo, tnw_piped)))
     return rc;
+  if ((rc = flush_deferred(c, c->xin))) return rc;   // (every path above has issued it already)
 
   if (out && (out->X || out->Y || out->Z)) {
     const long long n = (long long)R * D;
@@ -2247,6 +2345,7 @@ int dbsde_net_u(dbsde_ctx* c, const float* params, int R, const float* t, const 
   if ((rc = prep_weights(c, params))) return rc;
   const long long n = (long long)Rp * c->Dp;
   bool from_pf;
+  if ((rc = flush_deferred(c))) return rc;
   if ((rc = select_paths(c, nullptr, from_pf))) return rc;
   RUN(c, "netu_input", 0.0, 0.0,
       netu_input_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(t, X, R, D, c->Dp, c->xin));
@@ -2288,6 +2387,7 @@ int dbsde_net_u_vjp(dbsde_ctx* c, const float* params, int R, const float* t, co
   hipStream_t s = c->stream;
   if ((rc = prep_weights(c, params))) return rc;
   bool from_pf;
+  if ((rc = flush_deferred(c))) return rc;
   if ((rc = select_paths(c, nullptr, from_pf))) return rc;
   const long long n = (long long)Rp * c->Dp;
   const unsigned nb = (unsigned)((n + 255) / 256);
@@ -2307,6 +2407,7 @@ int dbsde_net_u_vjp(dbsde_ctx* c, const float* params, int R, const float* t, co
     RUN(c, "fused_fwd_inputgrad", 0.0, 0.0, kFused[fv].A<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));
     RUN(c, "fused_tangent_reverse", 0.0, 0.0, kFused[fv].C<<<Rp / WR, 64 * P3_WAVES, 0, s>>>(fa));
   } else {
+    if ((rc = flush_deferred(c, c->xin))) return rc;
     if ((rc = forward_and_inputgrad(c, R, Rp, false))) return rc;
     RUN(c, "vjp_cotangents", 0.0, 0.0,
         ext_cotan_kernel<<<nb, 256, 0, s>>>(ubar, zbar, R, Rp, D, c->Dp, c->u_clamp ? c->umask : nullptr, c->ubar,
@@ -2425,36 +2526,16 @@ int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
   if ((rc = ensure_rows(c, Rp, N))) return rc;
   for (int i = 0; i < 2; ++i)
     if (c->pend[i].valid && same_batch(c->pend[i].b, *next)) return DBSDE_OK;   // already queued
-  // a buffer no pending prefetch holds (else the older one's is replaced: its
-  // rollout is earlier on the same stream)
-  const int j = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
-  // after everything queued so far on the caller's stream (Xi ready, the
-  // buffer's previous readers done); work queued later overlaps this
-  if ((rc = stream_order(c, c->stream, c->pf_stream, ORD_PF_AFTER_MAIN))) return rc;
-  hipStream_t main_stream = c->stream;
-  float *xin0 = c->xin, *sdw0 = c->sdw;
-  c->stream = c->pf_stream;
-  c->xin = c->xin_b[j];
-  c->sdw = c->sdw_b[j];
-  hipError_t e = hipSuccess;
-  if (Rp > R) e = hipMemsetAsync(c->xin + (size_t)R * c->Dp, 0, (size_t)(Rp - R) * c->Dp * 4, c->stream);
-  if (e == hipSuccess) {
-    RolloutArgs ra = rollout_args(c, next);
-    ra.out = PATH_ROLLOUT;
-    rc = launch_paths(c, ra);
+  if (c->deferred && same_batch(c->defer_b, *next)) return DBSDE_OK;
+  if ((rc = flush_deferred(c))) return rc;
+  if (DBSDE_DEFER_PF && !c->heston && !c->Lt && c->pipe2) {
+    c->deferred = true;
+    c->defer_b = *next;
+    return DBSDE_OK;
   }
-  c->stream = main_stream;
-  c->xin = xin0;
-  c->sdw = sdw0;
-  if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("prefetch: ") + hipGetErrorString(e));
-  if (rc) return rc;
-  if ((rc = order_mark(c, ORD_PEND0 + j, c->pf_stream, c->pend[j].ready_v))) return rc;
-  c->pend[j].valid = true;
-  c->pend[j].joined = false;
-  c->pend[j].b = *next;
-  c->pend[j].seq = ++c->pf_seq;
-  return DBSDE_OK;
+  return issue_prefetch(c, next);
 }
+
 
 int dbsde_prefetch_cancel(dbsde_ctx* c) {
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
@@ -2467,6 +2548,7 @@ int dbsde_prefetch_cancel(dbsde_ctx* c) {
     if (rc) return rc;
   }
   c->pend[0].valid = c->pend[1].valid = false;
+  c->deferred = false;   // a held-back prefetch has issued no work
   return DBSDE_OK;
 }
 
