@@ -30,7 +30,7 @@
 #ifndef DBSDE_EVF
 #define DBSDE_EVF (hipEventDisableTiming | hipEventDisableSystemFence)
 #endif
-// a prefetched diagonal rollout runs on the next chunked step's second stream
+// a prefetched rollout runs on the next chunked step's second stream
 #ifndef DBSDE_DEFER_PF
 #define DBSDE_DEFER_PF 1
 #endif
@@ -2528,7 +2528,7 @@ int dbsde_prefetch(dbsde_ctx* c, const dbsde_batch* next) {
     if (c->pend[i].valid && same_batch(c->pend[i].b, *next)) return DBSDE_OK;   // already queued
   if (c->deferred && same_batch(c->defer_b, *next)) return DBSDE_OK;
   if ((rc = flush_deferred(c))) return rc;
-  if (DBSDE_DEFER_PF && !c->heston && !c->Lt && c->pipe2) {
+  if (DBSDE_DEFER_PF && c->pipe2) {
     c->deferred = true;
     c->defer_b = *next;
     return DBSDE_OK;
