@@ -2494,6 +2494,7 @@ int dbsde_set_corr(dbsde_ctx* c, const float* L, int n) {
   // a prefetched rollout read the old factor: drop it (and let it finish)
   if (c->pf_stream) HIPC(c, hipStreamSynchronize(c->pf_stream));
   c->pend[0].valid = c->pend[1].valid = false;
+  c->deferred = false;
   if (!L) {
     if (c->Lt) {
       HIPC(c, hipStreamSynchronize(c->stream));

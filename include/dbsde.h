@@ -187,14 +187,19 @@ int dbsde_brownian(dbsde_ctx* ctx, const dbsde_batch* batch, float* t, float* W,
  * Roll out a device-mode batch ahead of the dbsde_loss_grad that consumes it
  * (the reference's next fetch_minibatch, DeepBSDE.py:247-262, drawn while the
  * current iteration runs: train() draws each iteration's batch independently
- * of the model, nd_BSPDE_case.py:371).  The rollout runs on an internal
- * stream ordered after the work already queued on the context's stream, so
- * work queued later (the current iteration) overlaps it.  A later
+ * of the model, nd_BSPDE_case.py:371).  The batch is held back for the next
+ * dbsde_loss_grad / dbsde_train_step: if that step runs the two-stream phase
+ * pipeline, the rollout runs on its second stream after its weight-gradient
+ * work, ordered before the following step; otherwise (or at any other call
+ * that selects path buffers) it is issued then on an internal stream ordered
+ * after the work queued on the context's stream, and work queued later
+ * overlaps it.  A later
  * dbsde_loss_grad whose batch descriptor is identical (M, N, seed, offset,
  * path0, Xi pointer and rows; t = W = NULL) uses the prefetched paths instead
  * of rolling out; any other batch rolls out as usual.  At most two batches
- * are pending.  Xi is read when the prefetch runs: it must not change after
- * this call.  dbsde_set_corr drops pending prefetches.
+ * are pending.  Xi is read when the rollout runs: it must not change after
+ * this call until the batch is consumed or cancelled.  dbsde_set_corr drops
+ * pending prefetches.
  */
 int dbsde_prefetch(dbsde_ctx* ctx, const dbsde_batch* next);
 /* Forget every pending prefetch (e.g. the caller is about to rewrite the Xi
