@@ -7,7 +7,8 @@
     fresh one-chunk step bit for bit (no stale loss partial or weight-gradient
     row of the earlier batch is summed);
   * the streams ordered by value write / wait or by events give the same
-    training steps."""
+    training steps;
+  * a prefetch held back for the two-stream step changes no result."""
 import os
 
 import numpy as np
@@ -87,3 +88,25 @@ def test_stream_order_by_events_matches_value_ops(pkg, dev):
         runs.append(m.params.detach().cpu().clone())
     assert torch.isfinite(runs[0]).all()
     torch.testing.assert_close(runs[0], runs[1], rtol=0, atol=0)
+
+
+def test_held_back_prefetch_on_the_second_stream_is_the_same_step(pkg, dev):
+    """At the north-star shape the step runs the two-stream pipeline, so a
+    prefetched batch is held back and rolled out on the step's second stream
+    after its weight-gradient slices (engine.hip launch_deferred_on): four
+    device steps with the next batch prefetched end on the same parameters
+    bit for bit as four without prefetching; a prefetch that no step consumes
+    (a different seed) leaves the steps unchanged as well."""
+    g = _load("g2_north_star.npz")
+    runs = []
+    for mode in ("none", "next", "stale"):
+        m = _model(pkg, dev, g, {})
+        opt = m.new_optimizer_state("Adam", 1e-3)
+        for it in range(4):
+            nxt = {"none": None, "next": 22 + it, "stale": 1000 + it}[mode]
+            m.device_step(opt, 1e-3, seed=21 + it, next_seed=nxt)
+        torch.cuda.synchronize()
+        runs.append(m.params.detach().cpu().clone())
+    assert torch.isfinite(runs[0]).all()
+    torch.testing.assert_close(runs[1], runs[0], rtol=0, atol=0)
+    torch.testing.assert_close(runs[2], runs[0], rtol=0, atol=0)
