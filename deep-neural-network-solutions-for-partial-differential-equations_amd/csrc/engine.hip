@@ -1827,8 +1827,133 @@ namespace {
 // tangent along zbar and the reverse, then the weight-gradient contraction and
 // the finalize (+ the fused optimizer update).  Shared by loss_grad_impl and
 // the net_u VJP.
+// The chain layouts' weight-gradient problems over S_ row splits (split-bf16
+// tiles + the output-layer GEMV, or the fp32 split-K GEMM): arguments and
+// launch geometry, shared by the launch after the phase section and the
+// per-chunk launches inside the two-stream pipeline
+struct TNGeom {
+  int S_ = 0, maxt = 0, maxt3 = 0, rps32 = 0;
+  double tfl = 0.0;
+  float* oslab = nullptr;
+  long long sstride = 0;
+};
+int tn_setup(dbsde_ctx* c, int R, int Rp, TNArgs& ta, TNGeom& g) {
+  const auto& L = c->L;
+  const int K = c->K, S = c->Stot, D = c->D;
+  memset(&ta, 0, sizeof(ta));
+  // row splits for this batch: at least DBSDE_TN_SPLIT_ROWS rows each, at
+  // most the slab capacity; every kernel below covers all S_ splits, empty
+  // ones writing zeros, and the finalize sums exactly S_ of them
+  const int S_ = g.S_ = c->tn_splits_cur =
+      std::min(c->tn_splits, std::max(8, (Rp + DBSDE_TN_SPLIT_ROWS - 1) / DBSDE_TN_SPLIT_ROWS));
+  const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
+  ta.rows_per_split = rps;
+  ta.Rp = Rp;
+  double& tfl = g.tfl;
+  tfl = 0.0;
+  {
+    TNProb& p0 = ta.prob[0];
+    p0.A[0] = c->Alpha;
+    p0.lda[0] = S;
+    p0.nA[0] = c->Stot_x;
+    p0.B[0] = c->xin;
+    p0.ldb[0] = c->Dp;
+    p0.nB[0] = c->Dp;
+    p0.A[1] = c->Delta;
+    p0.lda[1] = S;
+    p0.nA[1] = c->Stot_x;
+    p0.B[1] = c->zbar;
+    p0.ldb[1] = c->Dp;
+    p0.nB[1] = c->Dp;
+    p0.npairs = 2;
+    p0.ones_col = -1;
+    p0.mv = c->slab_mv[0];
+    p0.nv = c->slab_nv[0];
+    p0.mt = c->slab_mt[0];
+    p0.nt = c->slab_nt[0];
+    p0.slab = c->slab[0];
+    int nv = 0;
+    for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
+    tfl += 2.0 * 2.0 * R * nv * (D + 2);
+  }
+  int& maxt = g.maxt;
+  maxt = ta.prob[0].mt * ta.prob[0].nt;
+  for (int j = 1; j <= K; ++j) {
+    TNProb& pj = ta.prob[j];
+    pj.A[0] = c->Alpha + c->col[j];
+    pj.lda[0] = S;
+    pj.nA[0] = c->Wp[j];
+    pj.B[0] = c->H + c->col[j - 1];
+    pj.ldb[0] = S;
+    pj.nB[0] = c->Wp[j - 1];
+    pj.A[1] = c->Delta + c->col[j];
+    pj.lda[1] = S;
+    pj.nA[1] = c->Wp[j];
+    pj.B[1] = c->Hdot + c->col[j - 1];
+    pj.ldb[1] = S;
+    pj.nB[1] = c->Wp[j - 1];
+    pj.npairs = 2;
+    pj.ones_col = c->has_v ? -1 : c->Wp[j - 1];
+    pj.mv = c->slab_mv[j];
+    pj.nv = c->slab_nv[j];
+    pj.mt = c->slab_mt[j];
+    pj.nt = c->slab_nt[j];
+    pj.slab = c->slab[j];
+    maxt = std::max(maxt, pj.mt * pj.nt);
+    tfl += 2.0 * 2.0 * R * L[j] * (L[j + 1] + (c->has_v ? 0 : 1));
+  }
+  {
+    // output layer: [w_out | b_out] = sum_r ubar_r [h_{K+1} | 1] + hdot_{K+1}
+    TNProb& po = ta.prob[K + 1];
+    po.A[0] = c->u16;
+    po.lda[0] = 16;
+    po.nA[0] = 16;
+    po.B[0] = c->H + c->col[K];
+    po.ldb[0] = S;
+    po.nB[0] = c->Wp[K];
+    po.A[1] = c->o16;
+    po.lda[1] = 16;
+    po.nA[1] = 16;
+    po.B[1] = c->Hdot + c->col[K];
+    po.ldb[1] = S;
+    po.nB[1] = c->Wp[K];
+    po.npairs = 2;
+    po.ones_col = c->Wp[K];
+    po.mv = 1;
+    po.nv = c->slab_nv[K + 1];
+    po.mt = c->slab_mt[K + 1];
+    po.nt = c->slab_nt[K + 1];
+    po.slab = c->slab[K + 1];
+    maxt = std::max(maxt, po.mt * po.nt);
+    tfl += 2.0 * 2.0 * R * (L[K + 1] + 1);
+  }
+  if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
+  if (c->tnx3) {
+    for (int j = 0; j <= K; ++j)
+      g.maxt3 = std::max(g.maxt3, ((ta.prob[j].nA[0] + TX_TILE - 1) / TX_TILE) * ((ta.prob[j].nB[0] + TX_TILE - 1) / TX_TILE));
+    g.rps32 = ((Rp + S_ - 1) / S_ + 31) / 32 * 32;
+    // tn_out_kernel's float4 loads at H + col[K] + r S: 16-byte aligned rows and column
+    if (Rp % 32 != 0 || c->Wp[K] % 4 != 0 || c->col[K] % 4 != 0 || S % 4 != 0)
+      return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
+    const TNProb& po = ta.prob[K + 1];
+    g.oslab = po.slab;
+    g.sstride = (long long)po.mt * 64 * po.nt * 64;
+  }
+  return DBSDE_OK;
+}
+// split-bf16 chain weight gradients of row splits [s0, s0 + sn) on stream st
+int tn_launch_splits(dbsde_ctx* c, int R, TNArgs ta, const TNGeom& g, int s0, int sn, hipStream_t st) {
+  const int K = c->K, S = c->Stot;
+  ta.split0 = s0;
+  tn_x3_kernel<<<dim3(g.maxt3, sn, K + 1), 256, 0, st>>>(ta, g.rps32);
+  tn_out_kernel<<<dim3(sn, (c->Wp[K] + 255) / 256), 1024, 0, st>>>(c->u16, c->H + c->col[K], c->Hdot + c->col[K], S,
+                                                                    c->Wp[K], R, g.rps32, g.oslab, g.sstride, s0);
+  HIPC(c, hipGetLastError());
+  return DBSDE_OK;
+}
+
 int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, float* grad, const double* loss_part,
-                  int nloss_parts, float* loss_dst, const FusedOpt* fo, bool tnw_piped) {
+                  int nloss_parts, float* loss_dst, const FusedOpt* fo, bool tnw_piped, bool tn_piped) {
   int rc;
   hipStream_t s = c->stream;
   const auto& L = c->L;
@@ -1916,112 +2041,20 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
     if (!tnw_piped && (rc = launch_tnw(c, R, Rp))) return rc;
     if ((rc = finalize_grads(c, params, grad, loss_part, nloss_parts, loss_dst, fo))) return rc;
   } else {
-  TNArgs ta;
-  memset(&ta, 0, sizeof(ta));
-  // row splits for this batch: at least DBSDE_TN_SPLIT_ROWS rows each, at
-  // most the slab capacity; every kernel below covers all S_ splits, empty
-  // ones writing zeros, and the finalize sums exactly S_ of them
-  const int S_ = c->tn_splits_cur =
-      std::min(c->tn_splits, std::max(8, (Rp + DBSDE_TN_SPLIT_ROWS - 1) / DBSDE_TN_SPLIT_ROWS));
-  const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
-  ta.rows_per_split = rps;
-  ta.Rp = Rp;
-  double tfl = 0.0;
-  {
-    TNProb& p0 = ta.prob[0];
-    p0.A[0] = c->Alpha;
-    p0.lda[0] = S;
-    p0.nA[0] = c->Stot_x;
-    p0.B[0] = c->xin;
-    p0.ldb[0] = c->Dp;
-    p0.nB[0] = c->Dp;
-    p0.A[1] = c->Delta;
-    p0.lda[1] = S;
-    p0.nA[1] = c->Stot_x;
-    p0.B[1] = c->zbar;
-    p0.ldb[1] = c->Dp;
-    p0.nB[1] = c->Dp;
-    p0.npairs = 2;
-    p0.ones_col = -1;
-    p0.mv = c->slab_mv[0];
-    p0.nv = c->slab_nv[0];
-    p0.mt = c->slab_mt[0];
-    p0.nt = c->slab_nt[0];
-    p0.slab = c->slab[0];
-    int nv = 0;
-    for (int j = 0; j <= (c->has_v ? K : 0); ++j) nv += L[j + 1];
-    tfl += 2.0 * 2.0 * R * nv * (D + 2);
-  }
-  int maxt = ta.prob[0].mt * ta.prob[0].nt;
-  for (int j = 1; j <= K; ++j) {
-    TNProb& pj = ta.prob[j];
-    pj.A[0] = c->Alpha + c->col[j];
-    pj.lda[0] = S;
-    pj.nA[0] = c->Wp[j];
-    pj.B[0] = c->H + c->col[j - 1];
-    pj.ldb[0] = S;
-    pj.nB[0] = c->Wp[j - 1];
-    pj.A[1] = c->Delta + c->col[j];
-    pj.lda[1] = S;
-    pj.nA[1] = c->Wp[j];
-    pj.B[1] = c->Hdot + c->col[j - 1];
-    pj.ldb[1] = S;
-    pj.nB[1] = c->Wp[j - 1];
-    pj.npairs = 2;
-    pj.ones_col = c->has_v ? -1 : c->Wp[j - 1];
-    pj.mv = c->slab_mv[j];
-    pj.nv = c->slab_nv[j];
-    pj.mt = c->slab_mt[j];
-    pj.nt = c->slab_nt[j];
-    pj.slab = c->slab[j];
-    maxt = std::max(maxt, pj.mt * pj.nt);
-    tfl += 2.0 * 2.0 * R * L[j] * (L[j + 1] + (c->has_v ? 0 : 1));
-  }
-  {
-    // output layer: [w_out | b_out] = sum_r ubar_r [h_{K+1} | 1] + hdot_{K+1}
-    TNProb& po = ta.prob[K + 1];
-    po.A[0] = c->u16;
-    po.lda[0] = 16;
-    po.nA[0] = 16;
-    po.B[0] = c->H + c->col[K];
-    po.ldb[0] = S;
-    po.nB[0] = c->Wp[K];
-    po.A[1] = c->o16;
-    po.lda[1] = 16;
-    po.nA[1] = 16;
-    po.B[1] = c->Hdot + c->col[K];
-    po.ldb[1] = S;
-    po.nB[1] = c->Wp[K];
-    po.npairs = 2;
-    po.ones_col = c->Wp[K];
-    po.mv = 1;
-    po.nv = c->slab_nv[K + 1];
-    po.mt = c->slab_mt[K + 1];
-    po.nt = c->slab_nt[K + 1];
-    po.slab = c->slab[K + 1];
-    maxt = std::max(maxt, po.mt * po.nt);
-    tfl += 2.0 * 2.0 * R * (L[K + 1] + 1);
-  }
-  if (K + 2 > 8) return fail(c, DBSDE_EINVAL, "internal: too many TN problems");
-  if (c->tnx3) {
-    // split-bf16 tiles for the layer problems (tnx3.hpp), a GEMV over the
-    // level-K tiles for the one-row output layer (tn_out_kernel; the fp32
-    // 64x64-tile GEMM took 58 us of HJB's 357)
-    int maxt3 = 0;
-    for (int j = 0; j <= K; ++j)
-      maxt3 = std::max(maxt3, ((ta.prob[j].nA[0] + TX_TILE - 1) / TX_TILE) * ((ta.prob[j].nB[0] + TX_TILE - 1) / TX_TILE));
-    const int rps32 = ((Rp + S_ - 1) / S_ + 31) / 32 * 32;
-    // tn_out_kernel's float4 loads at H + col[K] + r S: 16-byte aligned rows and column
-    if (Rp % 32 != 0 || c->Wp[K] % 4 != 0 || c->col[K] % 4 != 0 || S % 4 != 0)
-      return fail(c, DBSDE_EINVAL, "internal: tn x3 geometry");
-    const TNProb& po = ta.prob[K + 1];
-    const long long sstride = (long long)po.mt * 64 * po.nt * 64;
-    RUN(c, "tn_weight_grad", tfl, 0.0,
-        tn_x3_kernel<<<dim3(maxt3, S_, K + 1), 256, 0, s>>>(ta, rps32);
-        tn_out_kernel<<<dim3(S_, (c->Wp[K] + 255) / 256), 1024, 0, s>>>(c->u16, c->H + c->col[K], c->Hdot + c->col[K],
-                                                                         S, c->Wp[K], R, rps32, po.slab, sstride));
-  } else {
-    RUN(c, "tn_weight_grad", tfl, 0.0, tn_gemm_kernel<<<dim3(maxt, S_, K + 2), 256, 0, s>>>(ta));
+  if (!tn_piped) {
+    TNArgs ta;
+    TNGeom g;
+    if ((rc = tn_setup(c, R, Rp, ta, g))) return rc;
+    hipStream_t s = c->stream;
+    if (c->tnx3) {
+      const int S_ = g.S_, rps32 = g.rps32;
+      RUN(c, "tn_weight_grad", g.tfl, 0.0,
+          tn_x3_kernel<<<dim3(g.maxt3, S_, K + 1), 256, 0, s>>>(ta, rps32);
+          tn_out_kernel<<<dim3(S_, (c->Wp[K] + 255) / 256), 1024, 0, s>>>(c->u16, c->H + c->col[K], c->Hdot + c->col[K],
+                                                                           S, c->Wp[K], R, rps32, g.oslab, g.sstride, 0));
+    } else {
+      RUN(c, "tn_weight_grad", g.tfl, 0.0, tn_gemm_kernel<<<dim3(g.maxt, g.S_, K + 2), 256, 0, s>>>(ta));
+    }
   }
   if ((rc = finalize_grads(c, params, grad, loss_part, nloss_parts, loss_dst, fo))) return rc;
   }
@@ -2082,7 +2115,9 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   if (q3) RUN(c, "q3_sum", 0.0, 4.0 * M * N, q3_sum_kernel<<<N, 256, 0, s>>>(c->sdw, c->Dp, M, N, c->q3S));
 
   int nloss_parts;
-  bool tnw_piped = false;
+  bool tnw_piped = false, tn_piped = false;
+  TNArgs tn_a;
+  TNGeom tn_g;
   FusedArgs fa;
   c->tnw_S = tnw_slices(c, Rp);
   int fv = c->fv;
@@ -2146,7 +2181,19 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         // ms/step, profiles/r4_ab_chunks_piped.txt)
         tnw_piped = grad && c->tnw && !c->prof && np == 2 && nch == 2 && ok;
       }
-      if (!tnw_piped && (rc = flush_deferred(c, c->xin))) return rc;
+      // the chain layouts' split-bf16 weight gradients the same way: row
+      // splits of chunk 0 after its phase C on the main stream, the rest after
+      // chunk 1's on the second (the chunk boundary must be a split boundary)
+      int tn_s0 = 0;
+      if (grad && !c->tnw && c->tnx3 && !c->prof && np == 2 && nch == 2) {
+        if ((rc = tn_setup(c, R, Rp, tn_a, tn_g))) return rc;
+        const long long crow = (long long)cu[0] * utile * WR;
+        if (tn_g.rps32 > 0 && crow % tn_g.rps32 == 0 && crow / tn_g.rps32 < tn_g.S_) {
+          tn_s0 = (int)(crow / tn_g.rps32);
+          tn_piped = true;
+        }
+      }
+      if (!tnw_piped && !tn_piped && (rc = flush_deferred(c, c->xin))) return rc;
       hipStream_t ps[2] = {s, c->pipe2};
       if (np > 1 && (rc = stream_order(c, s, c->pipe2, ORD_FORK))) return rc;
       int t0 = 0;
@@ -2162,10 +2209,13 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         kFused[fv].A<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         kFused[fv].C<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         if (tnw_piped && (rc = launch_tnw(c, R, Rp, sb[i], sb[i + 1] - sb[i], st))) return rc;
+        if (tn_piped && (rc = tn_launch_splits(c, R, tn_a, tn_g, i == 0 ? 0 : tn_s0,
+                                               i == 0 ? tn_s0 : tn_g.S_ - tn_s0, st)))
+          return rc;
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());
-      if (tnw_piped && (rc = launch_deferred_on(c, c->pipe2))) return rc;
+      if ((tnw_piped || tn_piped) && (rc = launch_deferred_on(c, c->pipe2))) return rc;
       // the pending prefetched rollouts (the next step's paths, started a step
       // ago) are waited for on the second chunk stream, which finishes ahead of
       // the main one, so the join orders the main stream after them too and
@@ -2240,7 +2290,8 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
   if (!loss_in_fin)
     RUN(c, "loss_final", 0.0, 0.0, loss_final_kernel<<<1, 256, 0, s>>>(c->loss_part, nloss_parts, loss_dst));
 
-  if (grad && (rc = backward_tail(c, params, R, Rp, fv, grad, c->loss_part, nloss_parts, loss_dst, fo, tnw_piped)))
+  if (grad && (rc = backward_tail(c, params, R, Rp, fv, grad, c->loss_part, nloss_parts, loss_dst, fo, tnw_piped,
+                                  tn_piped)))
     return rc;
   if ((rc = flush_deferred(c, c->xin))) return rc;   // (every path above has issued it already)
 
@@ -2414,7 +2465,7 @@ int dbsde_net_u_vjp(dbsde_ctx* c, const float* params, int R, const float* t, co
                                             c->zbar, c->u16));
   }
   c->tnw_S = tnw_slices(c, Rp);
-  return backward_tail(c, params, R, Rp, fv, grad, nullptr, 0, nullptr, nullptr, false);
+  return backward_tail(c, params, R, Rp, fv, grad, nullptr, 0, nullptr, nullptr, false, false);
 }
 
 int dbsde_optimizer_step(dbsde_ctx* c, float* params, float* grad, float* m, float* v, const dbsde_optim* o) {

@@ -512,6 +512,7 @@ struct TNArgs {
   TNProb prob[8];
   int rows_per_split;
   int Rp;
+  int split0;   // tn_x3_kernel: first row split of this launch (piped per path chunk)
 };
 
 constexpr int TN_KC = 16;
@@ -926,8 +927,9 @@ __global__ void __launch_bounds__(256) netu_input_kernel(const float* t, const f
 // float4 column groups (a wave reads whole 1 KB rows), 8 rows in flight per
 // thread, the phases combined in a fixed order.  grid (splits, ceil(W / 256)).
 __global__ void __launch_bounds__(1024) tn_out_kernel(const float* u16, const float* H, const float* Hd, int ld,
-                                                      int W, int R, int rps, float* slab, long long sstride) {
-  const int s = blockIdx.x, t = threadIdx.x, cg = t & 63, ph = t >> 6;
+                                                      int W, int R, int rps, float* slab, long long sstride,
+                                                      int s0) {
+  const int s = s0 + (int)blockIdx.x, t = threadIdx.x, cg = t & 63, ph = t >> 6;
   const int c = blockIdx.y * 256 + 4 * cg;
   const bool cin = c < W;   // W % 4 == 0
   const int r0 = s * rps, r1 = min(r0 + rps, R);

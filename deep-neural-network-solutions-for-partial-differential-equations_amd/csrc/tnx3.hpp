@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(256, DBSDE_TNX3_WAVES) tn_x3_kernel(TNArgs arg
   int lin = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
   const int per = nx * ny * gridDim.z / 8;
   if (DBSDE_TNX3_XCD && lin < 8 * per) lin = (lin & 7) * per + (lin >> 3);
-  const int tile = lin % nx, split = (lin / nx) % ny, prob = lin / (nx * ny);
+  const int tile = lin % nx, split = args.split0 + (lin / nx) % ny, prob = lin / (nx * ny);
   const TNProb& P = args.prob[prob];
   const int tiles_n = (P.nB[0] + TX_TILE - 1) / TX_TILE, tiles_m = (P.nA[0] + TX_TILE - 1) / TX_TILE;
   if (tile >= tiles_m * tiles_n) return;

@@ -8,7 +8,9 @@
     row of the earlier batch is summed);
   * the streams ordered by value write / wait or by events give the same
     training steps;
-  * a prefetch held back for the two-stream step changes no result."""
+  * a prefetch held back for the two-stream step changes no result;
+  * the chain weight gradients piped per path chunk (HJB shape) give the
+    one-chunk step bit for bit."""
 import os
 
 import numpy as np
@@ -110,3 +112,37 @@ def test_held_back_prefetch_on_the_second_stream_is_the_same_step(pkg, dev):
     assert torch.isfinite(runs[0]).all()
     torch.testing.assert_close(runs[1], runs[0], rtol=0, atol=0)
     torch.testing.assert_close(runs[2], runs[0], rtol=0, atol=0)
+
+
+def test_chain_weight_gradients_piped_per_chunk(pkg, dev):
+    """Config 4's shape (HJB, FC-Sine [101,256x4,1], M = 2048, N = 20) runs
+    the two-chunk pipeline, and its split-bf16 chain weight gradients are
+    launched per chunk (row splits of chunk 0 after its phase C, the rest
+    after chunk 1's): the step is bit for bit the one-chunk step whose
+    weight gradients run after the phase section."""
+    D, M, N = 100, 2048, 20
+    layers = [D + 1] + 4 * [256] + [1]
+    rs = np.random.RandomState(41)
+    params = None
+    Xi = torch.zeros(D, device=dev)
+    res = []
+    for chunks in ("2", "1"):
+        old = os.environ.get("DBSDE_CHUNKS")
+        os.environ["DBSDE_CHUNKS"] = chunks
+        try:
+            s = pkg.NativeSolver("FC", layers, "Sine", pkg.ProblemSpec(sig_b=float(np.sqrt(2.0)), phi_zz=1.0, g="log"),
+                                 1.0, dev)
+        finally:
+            if old is None:
+                os.environ.pop("DBSDE_CHUNKS", None)
+            else:
+                os.environ["DBSDE_CHUNKS"] = old
+        if params is None:
+            params = torch.from_numpy(rs.normal(scale=0.05, size=s.nparams).astype(np.float32)).to(dev)
+        grad, loss = torch.empty_like(params), torch.empty(1, device=dev)
+        s.loss_grad(params, M, N, Xi, seed=9, grad=grad, loss=loss)
+        torch.cuda.synchronize()
+        res.append((float(loss), grad.cpu().clone()))
+    assert np.isfinite(res[0][0])
+    assert res[0][0] == res[1][0]
+    torch.testing.assert_close(res[0][1], res[1][1], rtol=0, atol=0)
