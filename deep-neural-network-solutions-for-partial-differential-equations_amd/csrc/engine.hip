@@ -1837,15 +1837,26 @@ struct TNGeom {
   float* oslab = nullptr;
   long long sstride = 0;
 };
-int tn_setup(dbsde_ctx* c, int R, int Rp, TNArgs& ta, TNGeom& g) {
+// align > 0 (split-bf16 form): the row count of the first path chunk, which
+// must then end on a split boundary -- when the default split does not, the
+// largest 32-row multiple no longer than it that divides align is taken
+int tn_setup(dbsde_ctx* c, int R, int Rp, TNArgs& ta, TNGeom& g, long long align = 0) {
   const auto& L = c->L;
   const int K = c->K, S = c->Stot, D = c->D;
   memset(&ta, 0, sizeof(ta));
   // row splits for this batch: at least DBSDE_TN_SPLIT_ROWS rows each, at
   // most the slab capacity; every kernel below covers all S_ splits, empty
   // ones writing zeros, and the finalize sums exactly S_ of them
-  const int S_ = g.S_ = c->tn_splits_cur =
-      std::min(c->tn_splits, std::max(8, (Rp + DBSDE_TN_SPLIT_ROWS - 1) / DBSDE_TN_SPLIT_ROWS));
+  int S_ = std::min(c->tn_splits, std::max(8, (Rp + DBSDE_TN_SPLIT_ROWS - 1) / DBSDE_TN_SPLIT_ROWS));
+  if (align > 0 && c->tnx3) {
+    int r32 = ((Rp + S_ - 1) / S_ + 31) / 32 * 32;
+    if (align % r32 != 0) {
+      for (r32 -= 32; r32 >= 32 && align % r32 != 0; r32 -= 32) {
+      }
+      if (r32 >= 32 && (Rp + r32 - 1) / r32 <= c->tn_splits) S_ = (Rp + r32 - 1) / r32;
+    }
+  }
+  g.S_ = c->tn_splits_cur = S_;
   const int rps = ((Rp + S_ - 1) / S_ + TN_KC - 1) / TN_KC * TN_KC;
   ta.rows_per_split = rps;
   ta.Rp = Rp;
@@ -2186,8 +2197,8 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       // chunk 1's on the second (the chunk boundary must be a split boundary)
       int tn_s0 = 0;
       if (grad && !c->tnw && c->tnx3 && !c->prof && np == 2 && nch == 2) {
-        if ((rc = tn_setup(c, R, Rp, tn_a, tn_g))) return rc;
         const long long crow = (long long)cu[0] * utile * WR;
+        if ((rc = tn_setup(c, R, Rp, tn_a, tn_g, crow))) return rc;
         if (tn_g.rps32 > 0 && crow % tn_g.rps32 == 0 && crow / tn_g.rps32 < tn_g.S_) {
           tn_s0 = (int)(crow / tn_g.rps32);
           tn_piped = true;
