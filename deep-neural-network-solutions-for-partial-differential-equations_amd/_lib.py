@@ -30,6 +30,7 @@ EXPORTED = [
     "dbsde_loss_grad", "dbsde_net_u", "dbsde_net_u_vjp", "dbsde_optimizer_step", "dbsde_exact", "dbsde_hjb_mc",
     "dbsde_profile_enable", "dbsde_profile_count", "dbsde_profile_read", "dbsde_profile_reset",
     "dbsde_vec_reduce", "dbsde_vec_axpby", "dbsde_lbfgs_direction", "dbsde_train_step",
+    "dbsde_stream_order_by_events",
 ]
 VEC_OPS = {"dot": 0, "asum": 1, "amax": 2}
 
@@ -89,6 +90,7 @@ def load():
         "dbsde_destroy": (None, [vp]),
         "dbsde_last_error": (ctypes.c_char_p, [vp]),
         "dbsde_set_stream": (i, [vp, vp]),
+        "dbsde_stream_order_by_events": (i, [ctypes.POINTER(ctypes.c_char_p)]),
         "dbsde_param_count": (ll, [vp]),
         "dbsde_param_used_mask": (i, [vp, vp, ll]),
         "dbsde_matrix_form": (i, [vp]),

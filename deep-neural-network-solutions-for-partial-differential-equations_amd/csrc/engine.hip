@@ -34,6 +34,11 @@
 #ifndef DBSDE_DEFER_PF
 #define DBSDE_DEFER_PF 1
 #endif
+// device-mode diagonal rollout: draws spread over the time steps
+// (rollout_steps_kernel; 0 = one thread per (path, column group) for all steps)
+#ifndef DBSDE_RS
+#define DBSDE_RS 1
+#endif
 // chunk fork / join through stream memory operations (stream_order)
 #ifndef DBSDE_MEMOPS
 #define DBSDE_MEMOPS 1
@@ -100,9 +105,12 @@ struct dbsde_ctx {
     dbsde_batch b{};
     hipEvent_t ready = nullptr;
     unsigned long long ready_v = 0;   // its order_mark token
-    // the caller's stream is already ordered after this rollout (the second
-    // chunk stream waited for it before the join), so its consumer need not wait
+    // joined_to is already ordered after this rollout (the second chunk stream
+    // waited for it before its join into joined_to), so a consumer on that
+    // stream need not wait; a consumer on any other stream (dbsde_set_stream
+    // may have swapped it) waits for the ready mark
     bool joined = false;
+    hipStream_t joined_to = nullptr;
     unsigned long long seq = 0;   // issue order: the older pending slot is the one replaced / reused
   } pend[2];
   unsigned long long pf_seq = 0;
@@ -113,6 +121,7 @@ struct dbsde_ctx {
   dbsde_batch defer_b{};
   hipStream_t pf_stream = nullptr;
   hipEvent_t ev_pf_order = nullptr;
+  hipEvent_t ev_switch = nullptr;   // dbsde_set_stream: the new stream after the old one
   // path-chunked phase pipeline: chunk i runs phase A then phase C on stream
   // (main, pipe2)[i % 2], so one chunk's phase C fills the other's phase-A tail.
   // The context creates only the streams it uses (pipe2, pf_stream): a process
@@ -258,17 +267,48 @@ int dalloc_t(dbsde_ctx* c, T** p, size_t n) {
 // A value wait is a kernel that spins until the value arrives, so it needs
 // the writer's queue to make progress beside it: anything that runs one kernel
 // at a time (kernel serialisation, launch blocking, rocprofv3 counter
-// collection) would never run the write.  Those environments, and
-// DBSDE_STREAM_ORDER=events, order the streams with events instead.
-bool env_set(const char* n) {
-  const char* v = getenv(n);
+// collection) would never run the write.  Those environments, any profiler /
+// tool library the runtime loads (HSA_TOOLS_LIB, a preloaded rocprof library,
+// ROCPROFILER_* / ROCP_* settings) and DBSDE_STREAM_ORDER=events order the
+// streams with events instead; DBSDE_STREAM_ORDER=values forces value ops.
+// Returns the reason (nullptr: value operations).
+// (env: a NULL-terminated NAME=VALUE block, nullptr = the process environment)
+const char* env_get(const char* const* env, const char* n) {
+  if (!env) return getenv(n);
+  const size_t k = strlen(n);
+  for (; *env; ++env)
+    if (!strncmp(*env, n, k) && (*env)[k] == '=') return *env + k + 1;
+  return nullptr;
+}
+bool env_set(const char* n, const char* const* env = nullptr) {
+  const char* v = env_get(env, n);
   return v && v[0] && strcmp(v, "0") != 0 && strcasecmp(v, "false") != 0;
 }
-bool order_by_events() {
-  if (const char* v = getenv("DBSDE_STREAM_ORDER"))
-    if (strcmp(v, "events") == 0) return true;
-  return env_set("AMD_SERIALIZE_KERNEL") || env_set("HIP_LAUNCH_BLOCKING") || env_set("ROCPROF_COUNTER_COLLECTION") ||
-         env_set("ROCPROF_COUNTERS");
+extern "C" char** environ;
+const char* events_reason(const char* const* env = nullptr) {
+  if (const char* v = env_get(env, "DBSDE_STREAM_ORDER")) {
+    if (strcmp(v, "events") == 0) return "DBSDE_STREAM_ORDER=events";
+    if (strcmp(v, "values") == 0) return nullptr;
+  }
+  static const char* const serial[] = {"AMD_SERIALIZE_KERNEL", "HIP_LAUNCH_BLOCKING", "ROCPROF_COUNTER_COLLECTION",
+                                       "ROCPROF_COUNTERS", "HSA_TOOLS_LIB"};
+  for (const char* n : serial)
+    if (env_set(n, env)) return n;
+  if (const char* p = env_get(env, "LD_PRELOAD"))
+    if (strstr(p, "rocprof")) return "LD_PRELOAD (rocprof)";
+  for (const char* const* e = env ? env : environ; e && *e; ++e)
+    if (!strncmp(*e, "ROCPROFILER_", 12) || !strncmp(*e, "ROCP_", 5)) return "ROCPROFILER_* / ROCP_* setting";
+  return nullptr;
+}
+bool order_by_events() { return events_reason() != nullptr; }
+// stderr line naming the ordering the first context chose (once per process)
+void log_ordering(bool memops) {
+  static bool done = false;
+  if (done || env_set("DBSDE_QUIET")) return;
+  done = true;
+  const char* why = events_reason();
+  fprintf(stderr, "dbsde: cross-stream order by %s%s%s\n", memops ? "stream value operations" : "events",
+          why ? " -- " : (memops ? "" : " -- value waits unsupported by the device"), why ? why : "");
 }
 
 // Cross-stream order points: order_mark(slot, from) marks `from`'s current
@@ -277,13 +317,14 @@ bool order_by_events() {
 // already enqueued, so it never lacks its write.  Slots: the chunk fork and
 // join, the prefetch stream after the caller's stream and back, the two
 // prefetch buffers' rollouts.
-enum { ORD_FORK = 0, ORD_JOIN = 1, ORD_PF_AFTER_MAIN = 2, ORD_MAIN_AFTER_PF = 3, ORD_PEND0 = 4 };
+enum { ORD_FORK = 0, ORD_JOIN = 1, ORD_PF_AFTER_MAIN = 2, ORD_MAIN_AFTER_PF = 3, ORD_PEND0 = 4, ORD_SWITCH = 6 };
 hipEvent_t order_event(dbsde_ctx* c, int slot) {
   switch (slot) {
     case ORD_FORK: return c->ev_pipe[0];
     case ORD_JOIN: return c->ev_pipe[1];
     case ORD_PF_AFTER_MAIN:
     case ORD_MAIN_AFTER_PF: return c->ev_pf_order;
+    case ORD_SWITCH: return c->ev_switch;
     default: return c->pend[slot - ORD_PEND0].ready;
   }
 }
@@ -835,7 +876,9 @@ int ensure_rows(dbsde_ctx* c, int Rp, int N) {
   if (!c->row_allocs.empty()) {
     HIPC(c, hipStreamSynchronize(c->stream));
     if (c->pf_stream) HIPC(c, hipStreamSynchronize(c->pf_stream));
+    if (c->pipe2) HIPC(c, hipStreamSynchronize(c->pipe2));
     c->pend[0].valid = c->pend[1].valid = false;
+    c->deferred = false;
     for (void* p : c->row_allocs) {
       (void)hipFree(p);
       c->allocs.erase(std::find(c->allocs.begin(), c->allocs.end(), p));
@@ -1006,6 +1049,10 @@ int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
     if (ra.ldx > CP_SROW) return fail(c, DBSDE_EINVAL, "internal: correlated rollout row staging");
     RUN(c, name, 2.0 * steps * ra.nb * ra.nb / 2, bytes,
         launch_corr(ra, s));
+  } else if (DBSDE_RS && ra.out == PATH_ROLLOUT && !ra.W && ra.ldx % 4 == 0) {
+    // device-mode increments: draws spread over the time steps (paths.hpp)
+    const long long pairs = (long long)ra.M * (ra.ldx / 4);
+    RUN(c, name, 0.0, bytes, rollout_steps_kernel<<<(unsigned)((pairs + RS_PAIRS - 1) / RS_PAIRS), RS_THREADS, 0, s>>>(ra));
   } else if (ra.out == PATH_ROLLOUT && ra.ldx % 4 == 0) {
     const int nthr = ra.M * (ra.ldx / 4);   // whole-row float4 stores
     RUN(c, name, 0.0, bytes, rollout4_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
@@ -1073,7 +1120,9 @@ int launch_deferred_on(dbsde_ctx* c, hipStream_t st) {
   int j = -1;
   for (int i = 0; i < 2 && j < 0; ++i)
     if (c->xin_b[i] != c->xin && !c->pend[i].valid) j = i;
-  if (j < 0) return flush_deferred(c);
+  // no free buffer: issue it on pf_stream, never into the buffer this step's
+  // queued kernels read (the older pending buffer is replaced instead)
+  if (j < 0) return flush_deferred(c, c->xin);
   c->deferred = false;
   const dbsde_batch nb = c->defer_b;
   const int R = nb.M * (nb.N + 1), Rp = (R + ROW_PAD - 1) / ROW_PAD * ROW_PAD;
@@ -1097,9 +1146,20 @@ int launch_deferred_on(dbsde_ctx* c, hipStream_t st) {
   if (rc) return rc;
   c->pend[j].valid = true;
   c->pend[j].joined = true;
+  c->pend[j].joined_to = c->stream;
   c->pend[j].b = nb;
   c->pend[j].seq = ++c->pf_seq;
   return DBSDE_OK;
+}
+
+// order the context stream after pending rollout i: its ready mark, or, for a
+// rollout joined into another stream (dbsde_set_stream changed it since), the
+// latest chunk join (written on pipe2 after the rollout was ordered there)
+int wait_pending(dbsde_ctx* c, int i) {
+  const auto& p = c->pend[i];
+  if (!p.joined) return order_wait(c, ORD_PEND0 + i, p.ready_v, c->stream);
+  if (p.joined_to == c->stream) return DBSDE_OK;
+  return order_wait(c, ORD_JOIN, c->order_epoch[ORD_JOIN], c->stream);
 }
 
 // Point c->xin / c->sdw at the path buffer this call uses.  A device-mode
@@ -1119,12 +1179,12 @@ int select_paths(dbsde_ctx* c, const dbsde_batch* b, bool& from_pf) {
     // a buffer no prefetch holds; both pending and neither is this batch: the
     // older one's buffer is reused once its rollout is done
     use = !c->pend[0].valid ? 0 : (!c->pend[1].valid ? 1 : (c->pend[0].seq <= c->pend[1].seq ? 0 : 1));
-    if (c->pend[use].valid && !c->pend[use].joined) {
-      const int rc = order_wait(c, ORD_PEND0 + use, c->pend[use].ready_v, c->stream);
+    if (c->pend[use].valid) {
+      const int rc = wait_pending(c, use);
       if (rc) return rc;
     }
-  } else if (!c->pend[use].joined) {
-    const int rc = order_wait(c, ORD_PEND0 + use, c->pend[use].ready_v, c->stream);
+  } else {
+    const int rc = wait_pending(c, use);
     if (rc) return rc;
   }
   c->pend[use].valid = false;
@@ -1763,12 +1823,14 @@ int dbsde_create(const dbsde_config* cfg, dbsde_ctx** out) {
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_pf_order, DBSDE_EVF);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_switch, DBSDE_EVF);
     for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pend[i].ready, DBSDE_EVF);
     if (e != hipSuccess) rc = fail(c, DBSDE_EHIP, std::string("side stream: ") + hipGetErrorString(e));
     int wv = 0;
     if (!rc && DBSDE_MEMOPS && !order_by_events() &&
         hipDeviceGetAttribute(&wv, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess && wv)
       c->memops = (rc = dalloc_t(c, &c->d_order, 8)) == DBSDE_OK;
+    if (!rc) log_ordering(c->memops);
   }
   if (rc) {
     g_last_error = c->err;
@@ -1789,6 +1851,7 @@ void dbsde_destroy(dbsde_ctx* c) {
     (void)hipStreamDestroy(c->pf_stream);
   }
   if (c->ev_pf_order) (void)hipEventDestroy(c->ev_pf_order);
+  if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
   for (int i = 0; i < 2; ++i) {
     if (c->pend[i].ready) (void)hipEventDestroy(c->pend[i].ready);
     if (c->ev_pipe[i]) (void)hipEventDestroy(c->ev_pipe[i]);
@@ -1806,9 +1869,21 @@ void dbsde_destroy(dbsde_ctx* c) {
 
 int dbsde_set_stream(dbsde_ctx* c, void* s) {
   if (!c) return fail(nullptr, DBSDE_EINVAL, "ctx is NULL");
-  c->stream = (hipStream_t)s;
+  const hipStream_t ns = (hipStream_t)s;
+  if (ns != c->stream && c->ev_switch) {
+    // the context's workspace (row buffers, pending rollouts, slabs) is
+    // written by the work already queued on the old stream: the new stream
+    // starts after it, so a caller may switch streams between calls without
+    // ordering them itself (no cost while the stream stays the same)
+    HIPC(c, hipSetDevice(c->device));
+    const int rc = stream_order(c, c->stream, ns, ORD_SWITCH);
+    if (rc) return rc;
+  }
+  c->stream = ns;
   return DBSDE_OK;
 }
+
+int dbsde_stream_order_by_events(const char* const* env) { return events_reason(env) ? 1 : 0; }
 
 long long dbsde_param_count(const dbsde_ctx* c) { return c ? c->nparams : -1; }
 
@@ -2232,9 +2307,12 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
       // the main one, so the join orders the main stream after them too and
       // the next step's phase A needs no wait of its own
       for (int i = 0; i < 2; ++i)
-        if (c->pend[i].valid && !c->pend[i].joined) {
-          if ((rc = order_wait(c, ORD_PEND0 + i, c->pend[i].ready_v, c->pipe2))) return rc;
+        if (c->pend[i].valid) {
+          // (a rollout joined before is already behind pipe2: the join below
+          // orders this step's stream after it)
+          if (!c->pend[i].joined && (rc = order_wait(c, ORD_PEND0 + i, c->pend[i].ready_v, c->pipe2))) return rc;
           c->pend[i].joined = true;
+          c->pend[i].joined_to = s;
         }
       if ((rc = stream_order(c, c->pipe2, s, ORD_JOIN))) return rc;
       if (c->prof) {
@@ -2610,6 +2688,13 @@ int dbsde_prefetch_cancel(dbsde_ctx* c) {
     const int rc = stream_order(c, c->pf_stream, c->stream, ORD_MAIN_AFTER_PF);
     if (rc) return rc;
   }
+  // (rollouts on the chunk stream are ordered by its join, into the stream
+  // they were joined to; another stream waits for the latest join)
+  for (int i = 0; i < 2; ++i)
+    if (c->pend[i].valid && c->pend[i].joined) {
+      const int rc = wait_pending(c, i);
+      if (rc) return rc;
+    }
   c->pend[0].valid = c->pend[1].valid = false;
   c->deferred = false;   // a held-back prefetch has issued no work
   return DBSDE_OK;

@@ -241,6 +241,119 @@ __global__ void __launch_bounds__(256) rollout4_kernel(RolloutArgs p) {
 }
 
 // --------------------------------------------------------------------------
+// Device-mode diagonal rollout with the draws spread over the time steps.
+// rollout4_kernel gives each (path, column group) pair one thread that draws
+// and steps all N steps in sequence: 28 x M threads, a 50-step chain of Philox
+// + Box-Muller + Euler per thread (latency-bound, 33 us at M = 1024 and at
+// M = 128).  Here a 256-thread workgroup owns 64 pairs: the Philox draws of a
+// 16-step window (64 pairs x 4 four-step blocks = 256 tasks, each the 4 live
+// dimensions of one block) go to an LDS buffer, and while waves 1-3 draw the
+// next window into the other buffer, wave 0 -- one lane per pair -- runs the
+// Euler recursion of the current window out of LDS and writes the whole xin /
+// sdw rows.  Per dimension every value is rollout4_kernel's (same Philox key,
+// same sqrt(dt) z, same non-contracted step, the same sequential fp64 time
+// grid), so X is bit-identical.
+// LDS: dw[buf][step in window][pair] as float4 (the pair's 4 columns):
+// lane-linear 16-byte reads, 2 x 16 KB.
+// --------------------------------------------------------------------------
+constexpr int RS_PAIRS = 64;
+constexpr int RS_THREADS = 256;
+constexpr int RS_WIN = 16;                       // steps per window (4 Philox blocks)
+
+__device__ __forceinline__ void rs_draw(const RolloutArgs& p, int g0, int C, int blk0, float sqdt, floatx4* buf,
+                                        int task) {
+  const int pr = task & (RS_PAIRS - 1), bw = task >> 6;   // pair, block within the window
+  const int g = g0 + pr, m = g / C, c = g - m * C;
+  const int b = blk0 + bw;
+  if (m >= p.M || 4 * b >= p.N) return;
+  float dw[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int d = 4 * c + k - 1;
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    if (d >= 0 && d < p.D) philox_normal4(p.seed, p.offset, (uint32_t)(p.path0 + m), (uint32_t)b, (uint32_t)d, z);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) dw[k][s] = sqdt * z[s];
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) buf[(4 * bw + s) * RS_PAIRS + pr] = floatx4{dw[0][s], dw[1][s], dw[2][s], dw[3][s]};
+}
+
+__global__ void __launch_bounds__(RS_THREADS) rollout_steps_kernel(RolloutArgs p) {
+  __shared__ floatx4 dws[2 * RS_WIN * RS_PAIRS];
+  const int C = p.ldx >> 2;
+  const int g0 = blockIdx.x * RS_PAIRS;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int N1 = p.N + 1, nsb = (p.N + 3) / 4, nw = (nsb + 3) / 4;
+  const float sqdt = sqrtf(p.T / (float)p.N);
+  const double dt64 = (double)p.T / (double)p.N;
+  // window 0: every thread draws one task
+  rs_draw(p, g0, C, 0, sqdt, dws, threadIdx.x);
+  __syncthreads();
+  // the chain lane's state (wave 0)
+  const int g = g0 + lane, m = g / C, c = g - m * C;
+  const bool ok = wave == 0 && m < p.M;
+  float x[4];
+  bool live[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int d = 4 * c + k - 1;
+    live[k] = d >= 0 && d < p.D;
+    x[k] = (ok && live[k]) ? p.Xi[(p.xi_rows == 1 ? 0 : m) * p.D + d] : 0.f;
+  }
+  double tacc = 0.0;
+  float t0 = (ok && p.t) ? p.t[(size_t)m * N1] : 0.0f;
+  for (int w = 0; w < nw; ++w) {
+    if (wave != 0) {
+      // the next window's 256 tasks over the 192 drawing threads
+      if (w + 1 < nw)
+        for (int task = threadIdx.x - 64; task < RS_WIN / 4 * RS_PAIRS; task += RS_THREADS - 64)
+          rs_draw(p, g0, C, 4 * (w + 1), sqdt, dws + ((w + 1) & 1) * RS_WIN * RS_PAIRS, task);
+    } else if (ok) {
+      const floatx4* buf = dws + (w & 1) * RS_WIN * RS_PAIRS;
+      for (int i = 0; i < RS_WIN; ++i) {
+        const int n = RS_WIN * w + i;
+        if (n >= p.N) break;
+        tacc += dt64;
+        const float t1 = p.t ? p.t[(size_t)m * N1 + n + 1] : (float)tacc;
+        const floatx4 dw = buf[i * RS_PAIRS + lane];
+        const float dt = rn_sub(t1, t0);
+        floatx4 xo, so;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int col = 4 * c + k;
+          float sv = 0.f;
+          if (live[k]) {
+            const float sg = rn_add(rn_mul(p.sig_a, x[k]), p.sig_b);
+            sv = rn_mul(sg, dw[k]);
+          }
+          xo[k] = col == 0 ? t0 : (col == p.D + 1 ? 1.f : x[k]);
+          so[k] = sv;
+          if (live[k]) x[k] = rn_add(rn_add(x[k], rn_mul(rn_mul(p.mu_a, x[k]), dt)), sv);
+        }
+        const size_t r = (size_t)m * N1 + n;
+        *(floatx4*)(p.xin + r * p.ldx + 4 * c) = xo;
+        *(floatx4*)(p.sdw + r * p.ldx + 4 * c) = so;
+        t0 = t1;
+      }
+    }
+    __syncthreads();
+  }
+  if (!ok) return;
+  floatx4 xo, so;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {   // n = N
+    const int col = 4 * c + k;
+    xo[k] = col == 0 ? t0 : (col == p.D + 1 ? 1.f : x[k]);
+    so[k] = 0.f;
+  }
+  const size_t r = (size_t)m * N1 + p.N;
+  *(floatx4*)(p.xin + r * p.ldx + 4 * c) = xo;
+  *(floatx4*)(p.sdw + r * p.ldx + 4 * c) = so;
+}
+
+// --------------------------------------------------------------------------
 // Cholesky-correlated device mode (with_corr...py:339-341: dW = L (sqrt(dt) z))
 // with the correlation product on the matrix cores: per step n the increments
 // of a 16-path group are dW^T = L . xi^T, one v_mfma_f32_16x16x4_f32 per

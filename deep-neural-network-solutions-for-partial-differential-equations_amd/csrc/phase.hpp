@@ -36,6 +36,19 @@
 
 namespace dbsde {
 
+// Timing-only ablations of the 64-row phase kernels (profiles/r6_ab_phase.txt;
+// results are wrong by construction, never built into the library): bit 0 no
+// s_barrier per piece, bit 1 no weight-gradient operand stores (H, Delta, Hdot,
+// Alpha, zbar), bit 2 no Abuf / G stores (phase C still loads them), bit 3 no
+// wait for the piece DMA, bit 4 no operand splits (one perm instead of the
+// hi / mid / lo split), bit 5 no LDS fragment reads (the piece's first
+// fragment reused); the weight-gradient operand stores: bit 6 cached instead
+// of non-temporal, bit 7 in tile order (1 KB contiguous per instruction),
+// bit 8 column-major 16 x 16 blocks (4 dword stores per block).
+#ifndef DBSDE_AB_PHASE
+#define DBSDE_AB_PHASE 0
+#endif
+
 constexpr int P3_WAVES = 4;
 constexpr int P3_ROWS = 16 * P3_WAVES;
 // split-bf16 weight ring depth: 3 pieces of 21 KiB (T = 7) per workgroup, two
@@ -64,6 +77,7 @@ __device__ __forceinline__ void bstore(const Mat<TT>& m, float* base, int ld, in
 // 64-byte row pieces.  Needs row0, col0, ld multiples of 16.
 template <int TT>
 __device__ __forceinline__ void fstore(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
+  if constexpr (DBSDE_AB_PHASE & 4) return;
   const int lane = threadIdx.x & 63;
   float* p = base + (size_t)row0 * ld + col0 * 16 + 4 * lane;
 #pragma unroll
@@ -83,10 +97,31 @@ __device__ __forceinline__ void fload(Mat<TT>& m, const float* base, int ld, int
 // (measured -13 us on the two phases, profiles/r2_ab_ntstore.txt)
 template <int TT>
 __device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
+  if constexpr (DBSDE_AB_PHASE & 2) return;
   const int lane = threadIdx.x & 63;
+  if constexpr (DBSDE_AB_PHASE & 128) {   // (ablation: tile order, 1 KB contiguous per instruction)
+    float* p = base + (size_t)row0 * ld + col0 * 16 + 4 * lane;
+#pragma unroll
+    for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 256 * t));
+    return;
+  }
+  if constexpr (DBSDE_AB_PHASE & 256) {   // (ablation: column-major 16x16 blocks, 4 dword stores)
+    const int cl = lane & 15, q = lane >> 4;
+    float* p = base + (size_t)row0 * ld + col0 * 16 + 64 * q + cl;
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) __builtin_nontemporal_store(m.v[t][r], p + 256 * t + 16 * r);
+    return;
+  }
   float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);
 #pragma unroll
-  for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 16 * t));
+  for (int t = 0; t < TT; ++t) {
+    if constexpr (DBSDE_AB_PHASE & 64)     // (ablation: cached stores)
+      *(floatx4*)(p + 16 * t) = m.v[t];
+    else
+      __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 16 * t));
+  }
 }
 
 // The LDS destination as a local-address-space pointer built from the low
@@ -114,7 +149,7 @@ __device__ __forceinline__ void vm_wait() {
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt / expcnt untouched
   asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  if constexpr (!(DBSDE_AB_PHASE & 1)) __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
 
@@ -246,7 +281,10 @@ struct PieceStagerT {
   }
   template <int NYOUNG>
   __device__ __forceinline__ const floatx4* next() {
-    if constexpr (NBUF > 2) {
+    if constexpr (DBSDE_AB_PHASE & 8) {
+    } else if constexpr (DBSDE_AB_PHASE & 6) {
+      vm_wait<0>();   // the removed stores no longer pad the counts: drain (errs slow)
+    } else if constexpr (NBUF > 2) {
       const int k = min(NBUF - 2, count() - 1 - st);
       wait_younger<NYOUNG, NBUF - 2>(k);
     } else {
@@ -312,6 +350,10 @@ struct Dw3 {
   unsigned h, m, l;
 };
 __device__ __forceinline__ Dw3 split_two(float x0, float x1) {
+  if constexpr (DBSDE_AB_PHASE & 16) {
+    const unsigned v = hi_pair(x0, x1);
+    return Dw3{v, v, v};
+  }
   const bf16x2 h = __builtin_convertvector(floatx2{x0, x1}, bf16x2);
   const float r0 = x0 - (float)h[0], r1 = x1 - (float)h[1];
   const bf16x2 m = __builtin_convertvector(floatx2{r0, r1}, bf16x2);
@@ -373,12 +415,13 @@ __device__ __forceinline__ void sgemm_x3_piece(Mat<TO>& acc, const Split3& s, co
   }
   SFor<0, TO>::run([&](auto oc) __attribute__((always_inline)) {
     constexpr int o = decltype(oc)::value;
+    constexpr int OR = (DBSDE_AB_PHASE & 32) ? 0 : 1;   // (ablation: every fragment read is fragment 0's)
     if constexpr (PF && o + 1 < TO) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) w[(o + 1) & 1][p] = im[(3 * (o + 1) + p) * 64 + lane];
+      for (int p = 0; p < 3; ++p) w[(o + 1) & 1][p] = im[(3 * (o + 1) * OR + p) * 64 + lane];
     } else if constexpr (!PF) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p) w[0][p] = im[(3 * o + p) * 64 + lane];
+      for (int p = 0; p < 3; ++p) w[0][p] = im[(3 * o * OR + p) * 64 + lane];
     }
     if constexpr (NEXT && o < 4) split_pair<TI, NEXT ? KBN : 0, o>(b, sn[0], sn[1], sn[2]);
     // in the order the fragment parts arrive (hi, mid, lo: counted lgkmcnt

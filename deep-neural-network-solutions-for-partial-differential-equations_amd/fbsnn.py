@@ -6,9 +6,11 @@ with_corr_high_dimension_pde.py:132-540 (v3: correlated increments) and,
 via deepbsde.FBSNN, DeepBSDE.py:140-323.  Same constructor arguments, method
 names, return types and attribute names; the work runs in the C ABI of
 include/dbsde.h (one context per GPU).  Subclasses declare their problem
-coefficients with `problem_spec()` (see problems.py); a subclass that only
-overrides phi_tf/g_tf/mu_tf/sigma_tf cannot run on the native path and is
-rejected at construction.
+coefficients with `problem_spec()` (see problems.py) and then run them in
+the kernels; a subclass that only overrides phi_tf/g_tf/mu_tf/sigma_tf (the
+reference's plugin API, nd_BSPDE_case.py:458-500), or overrides one that its
+inherited spec does not describe, runs its own methods through generic.py
+(its coefficients in torch, the network and the whole backward natively).
 
 Multi-GPU: when torch.distributed is initialised (one process per GPU), the
 M paths of every minibatch are split into contiguous blocks of M/world per
@@ -21,13 +23,14 @@ from __future__ import annotations
 
 import os
 import time
+import warnings
 from abc import ABC
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import networks
+from . import generic, networks
 from .solver import NativeSolver, ProblemSpec
 
 OPTIMIZER_NAMES = ("Adam", "SGD", "RMSprop", "AdamW", "Adadelta", "Adagrad", "Adamax", "ASGD", "LBFGS")
@@ -87,36 +90,49 @@ class _NetU(torch.autograd.Function):
 class _Loss(torch.autograd.Function):
     """FBSNN.loss_function's loss as a graph-connected scalar (the reference
     returns it with the graph built, DeepBSDE.py:278-279 / nd_BSPDE_case.py:378
-    call loss.backward() on it).  The forward is the forward-only native pass
-    (dbsde_loss_grad without a gradient), so a caller that only evaluates or
-    logs the loss pays no backward; it keeps the batch and a copy of the flat
-    parameters (0.37 MB at the north star), and the backward runs
-    dbsde_loss_grad on them -- the gradient of the weights the loss was
-    evaluated at, as the reference's saved graph gives even if the parameters
-    change in between -- scales it by the incoming cotangent and splits it
-    into the model parameters.  t, W and Xi are not differentiated; X and Y
-    are returned detached (a loss built from Y gets no gradient through it:
-    INTEGRATION.md)."""
+    call loss.backward() on it).  Until a backward has been seen on the
+    instance the forward is the forward-only native pass (dbsde_loss_grad
+    without a gradient), so a caller that only evaluates or logs the loss pays
+    no backward: it keeps the batch and a copy of the flat parameters (0.37 MB
+    at the north star), and the backward runs dbsde_loss_grad on them -- the
+    gradient of the weights the loss was evaluated at, as the reference's
+    saved graph gives even if the parameters change in between.  Once a
+    caller has called backward, later forwards compute loss and gradient in
+    one fused pass and the backward only scales it (no second forward, no
+    parameter copy).  The gradient is scaled by the incoming cotangent and
+    split into the model parameters.  t, W and Xi are not differentiated; X
+    and Y are returned detached (a loss built from Y gets no gradient through
+    it: INTEGRATION.md)."""
 
     @staticmethod
     def forward(ctx, fb, t, W, Xi, *params):
-        out = fb._run(t, W, Xi)
         ctx.fb = fb
-        ctx.batch = (t, W, Xi)
-        ctx.save_for_backward(fb.params.detach().clone())
+        if getattr(fb, "_loss_backward_seen", False):
+            g = torch.empty_like(fb.params)
+            out = fb._run(t, W, Xi, grad=g)
+            ctx.grad = g
+        else:
+            out = fb._run(t, W, Xi)
+            ctx.grad = None
+            ctx.batch = (t, W, Xi)
+            ctx.save_for_backward(fb.params.detach().clone())
         ctx.mark_non_differentiable(out["X"], out["Y"])
         return out["loss"][0].clone(), out["X"], out["Y"]
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, gl, gX, gY):
+        fb = ctx.fb
+        fb._loss_backward_seen = True
         if gl is None:
-            return (None,) * (4 + len(ctx.fb._param_slices()))
-        (snap,) = ctx.saved_tensors
-        t, W, Xi = ctx.batch
-        g = torch.empty_like(snap)
-        ctx.fb._run(t, W, Xi, grad=g, want=(), params=snap)
-        return (None, None, None, None) + ctx.fb._param_grads(g * gl.float())
+            return (None,) * (4 + len(fb._param_slices()))
+        g = ctx.grad
+        if g is None:
+            (snap,) = ctx.saved_tensors
+            t, W, Xi = ctx.batch
+            g = torch.empty_like(snap)
+            fb._run(t, W, Xi, grad=g, want=(), params=snap)
+        return (None, None, None, None) + fb._param_grads(g * gl.float())
 
 
 class FBSNN(ABC):
@@ -129,6 +145,8 @@ class FBSNN(ABC):
     log_every = 100              # nd_BSPDE_case.py:395,402 (with_corr / hjb: 500)
     log_print = True             # nd / hjb print the logged iterations (with_corr's print is commented out)
     train_returns_time_logs = False   # with_corr...py:453, hjb_implement.py:450 return 4 values
+    native_coefficients = True   # False: the subclass's own coefficient methods run (generic.py)
+    generic_reason = None        # why they do (set by _select_problem)
 
     def __init__(self, Xi, T, M, N, D, Mm, layers, mode, activation, correlation_type="no_correlation",
                  device=None):
@@ -138,11 +156,7 @@ class FBSNN(ABC):
         self.mode, self.activation = mode, activation
         self.layers = self._native_layers(list(layers))
         self.Xi = self._initial_state(Xi)
-        spec = self.problem_spec()
-        if not isinstance(spec, ProblemSpec):
-            raise NotImplementedError(
-                f"{type(self).__name__} does not declare problem_spec(); custom phi_tf/g_tf/mu_tf/"
-                "sigma_tf cannot run on the native path")
+        spec = self._select_problem()
         self.spec = spec
         self.solver = NativeSolver(mode, self.layers, activation, spec, T, self.device)
         self.model = self._make_model(list(layers))
@@ -176,6 +190,43 @@ class FBSNN(ABC):
 
     def problem_spec(self):
         return None
+
+    def _select_problem(self):
+        """The coefficients the native step runs.  A subclass whose
+        problem_spec() declares them, with every coefficient method it
+        overrides agreeing with that declaration on probe inputs, runs them in
+        the kernels (native_coefficients = True).  Any other subclass -- no
+        spec, the reference's way of defining a problem (nd_BSPDE_case.py:
+        458-500), or an override the inherited spec does not describe (e.g.
+        class MyBSB(BlackScholesBarenblatt) with its own sigma_tf) -- runs its
+        own methods through generic.py: its mu_tf / sigma_tf / phi_tf / g_tf /
+        Dg_tf in torch, the network and its whole backward natively.  Returns
+        the spec the native context is built with."""
+        spec = self.problem_spec()
+        why = None
+        if spec is not None and not isinstance(spec, ProblemSpec):
+            raise TypeError("problem_spec() must return a ProblemSpec or None")
+        if spec is None:
+            missing = [n for n in ("phi_tf", "g_tf") if generic.overridden(self, FBSNN, n) is None]
+            if missing:
+                raise NotImplementedError(f"{type(self).__name__} defines neither problem_spec() nor "
+                                          f"{' / '.join(missing)} (the reference's abstract methods)")
+            why = "no problem_spec()"
+        else:
+            bad = generic.coefficient_mismatches(self, FBSNN, spec, self.state_dim, self.T, self.Xi, self.device)
+            if bad and spec.kind != "diag":
+                raise NotImplementedError(f"{type(self).__name__} overrides {', '.join(bad)} of a {spec.kind!r} "
+                                          "problem; only DIAG-shaped problems run user coefficient methods")
+            if bad:
+                why = f"{', '.join(bad)} differ from the inherited problem_spec()"
+                warnings.warn(f"{type(self).__name__}: {why}; running the overridden methods (generic path)",
+                              stacklevel=3)
+        self.native_coefficients = why is None
+        self.generic_reason = why
+        if why is None:
+            return spec
+        generic.state_independence(self, self.state_dim, self.T, self.Xi, self.device)
+        return ProblemSpec(q3=True)     # the context's network only; the coefficients run in generic.py
 
     def phi_tf(self, t, X, Y, Z):
         raise NotImplementedError
@@ -259,6 +310,9 @@ class FBSNN(ABC):
         M, N1 = t.shape[0], t.shape[1]
         N, Ds, nb = N1 - 1, self.state_dim, self.solver.nb
         Xi = self._xi_rows(Xi, M)
+        if not self.native_coefficients:
+            return generic.loss_grad(self, self.params if params is None else params, t, W, Xi, grad=grad,
+                                     want=want, loss_out=loss)
         out = {"loss": torch.empty(1, device=self.device) if loss is None else loss}
         if "X" in want:
             out["X"] = torch.empty((M, N1, Ds), device=self.device)
@@ -544,6 +598,21 @@ class FBSNN(ABC):
         p0, ml = self._local_slice(self.M)
         xi = self._device_xi(p0, ml)
         lbfgs = opt_state["kind"] == "LBFGS"
+        if not self.native_coefficients:
+            # user coefficient methods (generic.py): the same device Philox
+            # increments, exported, then the generic loss and native backward
+            t, W = self.solver.brownian(ml, self.N, seed=seed, path0=p0)
+
+            def closure():
+                self._run(t, W, xi, grad=self.grad, want=(), loss=self._gradbuf[-1:])
+                return self._reduce()
+            loss = closure()
+            if lbfgs:
+                loss = loss.clone()
+                self._lbfgs_step(opt_state, lambda: float(closure().item()))
+                return loss
+            self._update(opt_state, learning_rate, skip_loss=loss if self.skip_nonfinite else None)
+            return loss
         if next_seed is not None and not lbfgs:
             self.solver.prefetch(ml, self.N, xi, seed=next_seed, path0=p0)
         if self.world == 1 and not lbfgs:

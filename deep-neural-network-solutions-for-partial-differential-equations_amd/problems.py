@@ -1,7 +1,9 @@
 """Problem classes of the reference, as FBSNN subclasses with native
 coefficients (problem_spec) plus the reference's torch expressions for
-phi_tf / g_tf / mu_tf / sigma_tf (API completeness; the native path does not
-call them).
+phi_tf / g_tf / mu_tf / sigma_tf.  The native step runs the spec; the methods
+are compared with it on probe inputs at construction (fbsnn._select_problem),
+so a subclass overriding one of them with other coefficients runs its own
+methods (generic.py) instead of silently training the parent's problem.
 
   CallOption            nd_BSPDE_case.py:503-539        sum-payoff call, phi = r(Y - X.Z)
   CallOption1D          1d_BSPDE_case.py:510-560        1-D call, phi = 0.01 Y (Q3 broadcast)

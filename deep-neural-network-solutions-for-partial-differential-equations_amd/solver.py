@@ -156,9 +156,13 @@ class NativeSolver:
 
     def prefetch(self, M, N, Xi, seed=0, offset=0, path0=0):
         """Roll out the device-mode batch a later loss_grad(M, N, Xi, seed=...,
-        offset=..., path0=...) with the same Xi tensor will consume, on an
-        internal stream overlapping the work queued after this call
-        (dbsde_prefetch).  Xi must stay unchanged (and alive) until then."""
+        offset=..., path0=...) with the same Xi tensor will consume
+        (dbsde_prefetch).  The rollout is held back until the next
+        loss_grad / train_step: a step running the two-stream phase pipeline
+        issues it on its second stream after its weight-gradient work, any
+        other call on an internal stream ordered after the work queued before
+        it.  Xi must stay unchanged (and alive) until the batch is consumed
+        or prefetch_drop() is called."""
         D = self.D
         self._check_tensor(Xi, "Xi")
         if Xi.numel() not in (D, M * D):

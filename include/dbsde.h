@@ -19,7 +19,10 @@
  *     save format), so torch checkpoints interoperate.
  *   - Work is enqueued on the stream set by dbsde_set_stream (default: the
  *     legacy null stream) and is asynchronous: results are valid once the
- *     stream has been synchronised.  The context keeps no caller pointer
+ *     stream has been synchronised.  Setting a different stream orders it
+ *     after the work already queued on the previous one (the context's
+ *     workspace is shared by its calls), so a caller may switch streams
+ *     between calls without synchronising.  The context keeps no caller pointer
  *     after a call returns.  A context is not thread safe.
  */
 #ifndef DBSDE_H
@@ -114,6 +117,21 @@ void dbsde_destroy(dbsde_ctx* ctx);
 const char* dbsde_last_error(const dbsde_ctx* ctx); /* ctx may be NULL */
 int dbsde_abi_version(void);
 int dbsde_set_stream(dbsde_ctx* ctx, void* hip_stream);
+
+/* No reference counterpart (the reference has one stream).  The context
+ * orders its internal streams with stream value operations (a wait spins
+ * until the writer's queue has run the write); under anything that runs one
+ * kernel at a time that wait would never end, so a context created in such an
+ * environment orders them with events.  Returns 1 when the current process
+ * environment selects events: DBSDE_STREAM_ORDER=events, AMD_SERIALIZE_KERNEL,
+ * HIP_LAUNCH_BLOCKING, ROCPROF_COUNTER_COLLECTION, ROCPROF_COUNTERS,
+ * HSA_TOOLS_LIB, an LD_PRELOAD naming rocprof, or any ROCPROFILER_* / ROCP_*
+ * variable (DBSDE_STREAM_ORDER=values overrides all of them); 0 otherwise.
+ * env: a NULL-terminated "NAME=VALUE" block to evaluate instead of the
+ * process environment (NULL = the process environment).  The first context
+ * of a process names its choice on stderr (DBSDE_QUIET=1 silences it).  Any
+ * other serialising tool needs DBSDE_STREAM_ORDER=events. */
+int dbsde_stream_order_by_events(const char* const* env);
 
 /* size of the flat parameter vector = sum of state_dict numels */
 long long dbsde_param_count(const dbsde_ctx* ctx);
