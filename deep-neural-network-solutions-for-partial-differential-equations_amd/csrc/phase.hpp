@@ -42,9 +42,9 @@ namespace dbsde {
 // Alpha, zbar), bit 2 no Abuf / G stores (phase C still loads them), bit 3 no
 // wait for the piece DMA, bit 4 no operand splits (one perm instead of the
 // hi / mid / lo split), bit 5 no LDS fragment reads (the piece's first
-// fragment reused); the weight-gradient operand stores: bit 6 cached instead
-// of non-temporal, bit 7 in tile order (1 KB contiguous per instruction),
-// bit 8 column-major 16 x 16 blocks (4 dword stores per block).
+// fragment reused); the operand stores of bstore_stream: bit 6 cached instead
+// of non-temporal, bit 7 tile order, bit 11 into LDS instead, bit 12 the even
+// blocks only.
 #ifndef DBSDE_AB_PHASE
 #define DBSDE_AB_PHASE 0
 #endif
@@ -95,28 +95,75 @@ __device__ __forceinline__ void fload(Mat<TT>& m, const float* base, int ld, int
 // both phases (H, Delta, Hdot, Alpha, zbar): no L2 allocate, so Abuf / G / zfull,
 // which phase C re-reads shortly after phase A wrote them, keep the cache
 // (measured -13 us on the two phases, profiles/r2_ab_ntstore.txt)
+// tile = true: the "column tile" layout instead (FusedArgs.optile; the
+// wave-owned weight-gradient kernel reads either, tnw.hpp op_off): in each
+// 16-row tile, every 16 x 16 block is 256 contiguous floats stored column by
+// column (element (r, c) at 16 c + r).  A quad transpose (DPP) turns the
+// lanes' row fragments into column fragments first, so every store
+// instruction writes one contiguous 1 KiB block instead of 64 bytes in each
+// of 16 rows, and the weight-gradient kernel reads a lane's 8 rows of one
+// column as two 16-byte loads.  The phase kernels' stores are issue-bound:
+// the 7.6 KB per row of these operands cost the phase section 0.12 ms against
+// 0.06 ms written to LDS instead; 1 KiB blocks take 38 us of it
+// (profiles/r6_ab_phase.txt).
+//
+// 4 x 4 transpose across the lanes of a quad: lane 4a + b's v[k] (element
+// (row 4a + b, col 4q + k) of a block) becomes element (row 4a + k,
+// col 4q + b), two butterfly stages of quad_perm DPP moves.
+template <int CTRL>
+__device__ __forceinline__ float qperm(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ floatx4 quad_transpose(floatx4 v) {
+  const int lane = threadIdx.x & 63;
+  const bool x = lane & 2, y = lane & 1;
+  // stage 1: the 2 x 2 blocks across lane bit 1 (quad_perm 2,3,0,1)
+  float r0 = qperm<0x4E>(x ? v[0] : v[2]), r1 = qperm<0x4E>(x ? v[1] : v[3]);
+  floatx4 w;
+  w[0] = x ? r0 : v[0];
+  w[1] = x ? r1 : v[1];
+  w[2] = x ? v[2] : r0;
+  w[3] = x ? v[3] : r1;
+  // stage 2: across lane bit 0 (quad_perm 1,0,3,2)
+  r0 = qperm<0xB1>(y ? w[0] : w[1]);
+  r1 = qperm<0xB1>(y ? w[2] : w[3]);
+  floatx4 o;
+  o[0] = y ? r0 : w[0];
+  o[1] = y ? w[1] : r0;
+  o[2] = y ? r1 : w[2];
+  o[3] = y ? w[3] : r1;
+  return o;
+}
 template <int TT>
-__device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
+__device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int ld, int row0, int col0,
+                                              bool tile = false) {
   if constexpr (DBSDE_AB_PHASE & 2) return;
   const int lane = threadIdx.x & 63;
-  if constexpr (DBSDE_AB_PHASE & 128) {   // (ablation: tile order, 1 KB contiguous per instruction)
+  if constexpr (DBSDE_AB_PHASE & 2048) {   // (ablation: into LDS instead, over the ring's first KB)
+#pragma unroll
+    for (int t = 0; t < TT; ++t) asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(16 * lane)), "v"(m.v[t]));
+    return;
+  }
+  if (tile) {
+    // lane (cl = 4a + b, q) holds column 4q + b, rows 4a .. 4a + 3 after the
+    // transpose: block offset 16 (4q + b) + 4a
+    const int cl = lane & 15;
+    float* p = base + (size_t)row0 * ld + col0 * 16 + 64 * (lane >> 4) + 16 * (cl & 3) + 4 * (cl >> 2);
+#pragma unroll
+    for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(quad_transpose(m.v[t]), (floatx4*)(p + 256 * t));
+    return;
+  }
+  if constexpr (DBSDE_AB_PHASE & 128) {   // (ablation: fstore's tile order, no transpose)
     float* p = base + (size_t)row0 * ld + col0 * 16 + 4 * lane;
 #pragma unroll
     for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 256 * t));
     return;
   }
-  if constexpr (DBSDE_AB_PHASE & 256) {   // (ablation: column-major 16x16 blocks, 4 dword stores)
-    const int cl = lane & 15, q = lane >> 4;
-    float* p = base + (size_t)row0 * ld + col0 * 16 + 64 * q + cl;
-#pragma unroll
-    for (int t = 0; t < TT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) __builtin_nontemporal_store(m.v[t][r], p + 256 * t + 16 * r);
-    return;
-  }
   float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
+    if constexpr (DBSDE_AB_PHASE & 4096)   // (ablation: the even blocks only)
+      if (t & 1) continue;
     if constexpr (DBSDE_AB_PHASE & 64)     // (ablation: cached stores)
       *(floatx4*)(p + 16 * t) = m.v[t];
     else
@@ -619,7 +666,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero(acc);
-    stage_mm<X3, T, T, T, T, PFA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd); });
+    stage_mm<X3, T, T, T, T, PFA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd, p.optile); });
     if constexpr (HV) stage_mm<X3, T, TD, 0, 0, PFA>(acc, x, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o) {
@@ -660,7 +707,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
     }
     if (q == 0) p.u[row0 + cl] = uv;
   }
-  bstore_stream(h, p.H, S, row0, K * Wd);
+  bstore_stream(h, p.H, S, row0, K * Wd, p.optile);
   // input gradient: g_{K+1} = w_out, delta_K = w_out act'(a_K)
   Mat<T> g, dl;
 #pragma unroll
@@ -680,7 +727,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
     constexpr int j = K - decltype(ic)::value;
     auto prev = [&]() __attribute__((always_inline)) {   // (g_j, delta_j) of the previous step
       if constexpr (j < K) fstore(g, p.G, S, row0, j * Wd);
-      bstore_stream(dl, p.Delta, S, row0, j * Wd);
+      bstore_stream(dl, p.Delta, S, row0, j * Wd, p.optile);
       if constexpr (RECOMP) fload(av, p.Abuf, S, row0, (j - 1) * Wd);
     };
     Mat<T> gn;
@@ -703,7 +750,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
   });
   stage_mm<X3, TD, T, 0, 2 * T + TD, PFA>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
     fstore(g, p.G, S, row0, 0);
-    bstore_stream(dl, p.Delta, S, row0, 0);
+    bstore_stream(dl, p.Delta, S, row0, 0, p.optile);
     bload(x, p.xin, p.Dp, row0, 0);
   });
   if (p.u_clamp) {
@@ -805,7 +852,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
                           : 0.f;
       }
   }
-  bstore_stream(zb, p.zbar, p.Dp, row0, 0);
+  bstore_stream(zb, p.zbar, p.Dp, row0, 0, p.optile);
   tz += __shfl_xor(tz, 16);
   tz += __shfl_xor(tz, 32);
   {
@@ -856,7 +903,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
     constexpr int j = decltype(jc)::value;
     if constexpr (!XFIRST) zero(ad[j]);
     stage_mm<X3, T, T, 0, 2 * T, PFC_T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
-      bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd);
+      bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd, p.optile);
       fload(av, p.Abuf, S, row0, j * Wd);
     });
     if constexpr (HV && !XFIRST) stage_mm<X3, T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
@@ -865,7 +912,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) hd.v[o][rr] = act_1<ACT>(av.v[o][rr]) * ad[j].v[o][rr] + p.rho * hd.v[o][rr];
   });
-  bstore_stream(hd, p.Hdot, S, row0, K * Wd);
+  bstore_stream(hd, p.Hdot, S, row0, K * Wd, p.optile);
   // reverse: p_{K+1} = ubar w_out ; alpha_K = w_out (ubar act'(a_K) + adot_K act''(a_K))
   Mat<T> pv, al;
   {
@@ -887,7 +934,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
     Mat<T> acc, gg;
     zero(acc);
     stage_mm<X3, T, T, 0, 3 * T, PFC_R>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
-      bstore_stream(al, p.Alpha, S, row0, j * Wd);
+      bstore_stream(al, p.Alpha, S, row0, j * Wd, p.optile);
       fload(av, p.Abuf, S, row0, (j - 1) * Wd);
       fload(gg, p.G, S, row0, (j - 1) * Wd);
     });
@@ -902,7 +949,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
         al.v[o][rr] = pp * d1 + gg.v[o][rr] * ad[j - 1].v[o][rr] * d2;
       }
   });
-  bstore_stream(al, p.Alpha, S, row0, 0);
+  bstore_stream(al, p.Alpha, S, row0, 0, p.optile);
 }
 
 }  // namespace dbsde

@@ -13,6 +13,7 @@ JSON.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import importlib
 import json
@@ -108,6 +109,11 @@ def main():
             samples.append(row)
             time.sleep(args.period * 1e-3)
 
+    # in-kernel clock between steps (tools/ubench/clockstamp.hip; build:
+    # hipcc -O3 --offload-arch=gfx950 -fPIC -shared -o tools/ubench/libclockstamp.so tools/ubench/clockstamp.hip)
+    cs_path = os.path.join(ROOT, "tools", "ubench", "libclockstamp.so")
+    cs = ctypes.CDLL(cs_path) if os.path.exists(cs_path) else None
+    stamps = torch.zeros(2 * (args.steps + 1), dtype=torch.int64, device=dev)
     th = threading.Thread(target=sampler, daemon=True)
     th.start()
     time.sleep(0.05)
@@ -124,6 +130,8 @@ def main():
     for k in range(args.steps):
         m.device_step(opt, 1e-3, seed=it, next_seed=it + 1)
         evs[k].record(stream)
+        if cs is not None:
+            cs.clockstamp_launch(ctypes.c_void_p(stamps.data_ptr()), k, ctypes.c_void_p(stream.cuda_stream))
         it += 1
     torch.cuda.synchronize()
     time.sleep(0.02)
@@ -135,12 +143,14 @@ def main():
     t_end = host0 + ends * 1e-3
     t_start = np.concatenate([[host0], t_end[:-1]])
     keys = sorted(files)
+    st = stamps.cpu().numpy().reshape(-1, 2)
     rows = []
     for k in range(args.steps):
         ss = [s for s in samples if t_start[k] <= s["t"] < t_end[k]]
         if not ss:   # nearest sample
             ss = [min(samples, key=lambda s: abs(s["t"] - 0.5 * (t_start[k] + t_end[k])))] if samples else []
-        r = {"step": k, "ms": float(dur[k]), "n_samples": len(ss)}
+        r = {"step": k, "ms": float(dur[k]), "n_samples": len(ss),
+             "kernel_mhz": float(100.0 * st[k, 0] / st[k, 1]) if cs is not None and st[k, 1] else None}
         for key in keys:
             v = [s[key] for s in ss if s.get(key) is not None]
             r[key] = float(np.mean(v)) if v else None
@@ -150,6 +160,8 @@ def main():
         a, b = (int(x) for x in w.split("-"))
         sel = [r for r in rows if a <= r["step"] <= b]
         summary[w] = {"ms_mean": float(np.mean([r["ms"] for r in sel]))}
+        km = [r["kernel_mhz"] for r in sel if r["kernel_mhz"]]
+        summary[w]["kernel_mhz"] = float(np.mean(km)) if km else None
         for key in keys:
             v = [r[key] for r in sel if r[key] is not None]
             summary[w][key] = float(np.mean(v)) if v else None
@@ -160,7 +172,8 @@ def main():
                    "sample_period_ms": args.period}, f, indent=1)
     print(json.dumps(summary))
     for r in rows:
-        print(r["step"], "%.1f us" % (1e3 * r["ms"]), " ".join(f"{k}={r[k]}" for k in keys))
+        print(r["step"], "%.1f us" % (1e3 * r["ms"]), "kernel_mhz=%s" % r["kernel_mhz"],
+              " ".join(f"{k}={r[k]}" for k in keys))
 
 
 if __name__ == "__main__":
