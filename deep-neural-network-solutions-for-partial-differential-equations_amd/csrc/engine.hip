@@ -34,10 +34,14 @@
 #ifndef DBSDE_DEFER_PF
 #define DBSDE_DEFER_PF 1
 #endif
-// the fused phase kernels write the weight-gradient operands in tile order
-// when the wave-owned tiles read them (phase.hpp bstore_stream)
+// the fused phase kernels write the weight-gradient operands in block tiles
+// (phase.hpp bstore_stream) when the wave-owned tiles read them: the phase
+// section gains 30-38 us (1 KiB contiguous stores), but the weight-gradient
+// kernel reading the same bytes from block tiles loses 35-58 us with the same
+// instruction stream (column tiles, block tiles, block-major orders:
+// profiles/r6_ab_phase.txt 5), so the default stays row-major
 #ifndef DBSDE_OPTILE
-#define DBSDE_OPTILE 1
+#define DBSDE_OPTILE 0
 #endif
 // device-mode diagonal rollout with the draws spread over the time steps
 // (rollout_steps_kernel, 1) or one thread per (path, column group) for all

@@ -95,45 +95,16 @@ __device__ __forceinline__ void fload(Mat<TT>& m, const float* base, int ld, int
 // both phases (H, Delta, Hdot, Alpha, zbar): no L2 allocate, so Abuf / G / zfull,
 // which phase C re-reads shortly after phase A wrote them, keep the cache
 // (measured -13 us on the two phases, profiles/r2_ab_ntstore.txt)
-// tile = true: the "column tile" layout instead (FusedArgs.optile; the
+// tile = true: the "block tile" layout instead (FusedArgs.optile; the
 // wave-owned weight-gradient kernel reads either, tnw.hpp op_off): in each
-// 16-row tile, every 16 x 16 block is 256 contiguous floats stored column by
-// column (element (r, c) at 16 c + r).  A quad transpose (DPP) turns the
-// lanes' row fragments into column fragments first, so every store
-// instruction writes one contiguous 1 KiB block instead of 64 bytes in each
-// of 16 rows, and the weight-gradient kernel reads a lane's 8 rows of one
-// column as two 16-byte loads.  The phase kernels' stores are issue-bound:
-// the 7.6 KB per row of these operands cost the phase section 0.12 ms against
-// 0.06 ms written to LDS instead; 1 KiB blocks take 38 us of it
-// (profiles/r6_ab_phase.txt).
-//
-// 4 x 4 transpose across the lanes of a quad: lane 4a + b's v[k] (element
-// (row 4a + b, col 4q + k) of a block) becomes element (row 4a + k,
-// col 4q + b), two butterfly stages of quad_perm DPP moves.
-template <int CTRL>
-__device__ __forceinline__ float qperm(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ floatx4 quad_transpose(floatx4 v) {
-  const int lane = threadIdx.x & 63;
-  const bool x = lane & 2, y = lane & 1;
-  // stage 1: the 2 x 2 blocks across lane bit 1 (quad_perm 2,3,0,1)
-  float r0 = qperm<0x4E>(x ? v[0] : v[2]), r1 = qperm<0x4E>(x ? v[1] : v[3]);
-  floatx4 w;
-  w[0] = x ? r0 : v[0];
-  w[1] = x ? r1 : v[1];
-  w[2] = x ? v[2] : r0;
-  w[3] = x ? v[3] : r1;
-  // stage 2: across lane bit 0 (quad_perm 1,0,3,2)
-  r0 = qperm<0xB1>(y ? w[0] : w[1]);
-  r1 = qperm<0xB1>(y ? w[2] : w[3]);
-  floatx4 o;
-  o[0] = y ? r0 : w[0];
-  o[1] = y ? w[1] : r0;
-  o[2] = y ? r1 : w[2];
-  o[3] = y ? w[3] : r1;
-  return o;
-}
+// 16-row tile, every 16 x 16 block is 1 KiB contiguous, row-major inside
+// (element (r, c) at 16 r + c).  A lane's float4 (row cl, columns 4q .. 4q + 3)
+// lands at 16 cl + 4 q, so one store instruction writes one whole block --
+// 1 KiB contiguous instead of 64 bytes in each of 16 rows -- and the
+// weight-gradient kernel still reads 64 contiguous bytes per row per
+// instruction.  The phase kernels' stores are issue-bound: the 7.6 KB per row
+// of these operands cost the phase section 0.12 ms against 0.06 ms written to
+// LDS instead (profiles/r6_ab_phase.txt).
 template <int TT>
 __device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int ld, int row0, int col0,
                                               bool tile = false) {
@@ -145,12 +116,9 @@ __device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int
     return;
   }
   if (tile) {
-    // lane (cl = 4a + b, q) holds column 4q + b, rows 4a .. 4a + 3 after the
-    // transpose: block offset 16 (4q + b) + 4a
-    const int cl = lane & 15;
-    float* p = base + (size_t)row0 * ld + col0 * 16 + 64 * (lane >> 4) + 16 * (cl & 3) + 4 * (cl >> 2);
+    float* p = base + (size_t)row0 * ld + col0 * 16 + 16 * (lane & 15) + 4 * (lane >> 4);
 #pragma unroll
-    for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(quad_transpose(m.v[t]), (floatx4*)(p + 256 * t));
+    for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 256 * t));
     return;
   }
   if constexpr (DBSDE_AB_PHASE & 128) {   // (ablation: fstore's tile order, no transpose)

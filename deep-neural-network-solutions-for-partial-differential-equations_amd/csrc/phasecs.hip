@@ -48,15 +48,14 @@ __device__ __forceinline__ void fload_n(Mat<2>& m, const float* base, int ld, in
   m.v[0] = *(const floatx4*)p;
   m.v[1] = *(const floatx4*)(p + (n > 1 ? 256 : 0));
 }
-// (tile: phase.hpp bstore_stream's column tiles, FusedArgs.optile)
+// (tile: phase.hpp bstore_stream's block tiles, FusedArgs.optile)
 __device__ __forceinline__ void bstore_stream_n(const Mat<2>& m, float* base, int ld, int row0, int col0, int n,
                                                 bool tile) {
   const int lane = threadIdx.x & 63;
-  if (tile) {   // (phase.hpp bstore_stream: column tiles through a quad transpose)
-    const int cl = lane & 15;
-    float* p = base + (size_t)row0 * ld + col0 * 16 + 64 * (lane >> 4) + 16 * (cl & 3) + 4 * (cl >> 2);
-    __builtin_nontemporal_store(quad_transpose(m.v[0]), (floatx4*)p);
-    __builtin_nontemporal_store(quad_transpose(pick(n > 1, m.v[1], m.v[0])), (floatx4*)(p + (n > 1 ? 256 : 0)));
+  if (tile) {   // (phase.hpp bstore_stream: block tiles)
+    float* p = base + (size_t)row0 * ld + col0 * 16 + 16 * (lane & 15) + 4 * (lane >> 4);
+    __builtin_nontemporal_store(m.v[0], (floatx4*)p);
+    __builtin_nontemporal_store(pick(n > 1, m.v[1], m.v[0]), (floatx4*)(p + (n > 1 ? 256 : 0)));
     return;
   }
   float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);

@@ -32,9 +32,9 @@ struct TNWProb {
   const float* A2;
   const float* B2;
   int lda1, ldb1, lda2, ldb2;
-  // operand layouts: 0 row-major [rows, ld]; 1 column tiles (phase.hpp
+  // operand layouts: 0 row-major [rows, ld]; 1 block tiles (phase.hpp
   // bstore_stream: each 16 x 16 block of a 16-row tile is 256 contiguous
-  // floats, element (row, col) of the block at 16 col + row) -- the fused
+  // floats, row-major inside, element (row, col) at 16 row + col) -- the fused
   // phase kernels write the weight-gradient operands that way.  A1 and A2
   // share ta.
   int ta, tb1, tb2;
@@ -45,7 +45,7 @@ struct TNWProb {
 template <bool TILE>
 __device__ __forceinline__ size_t op_off(int row, int col, int ld) {
   if constexpr (!TILE) return (size_t)row * ld + col;
-  return (size_t)(row >> 4) * 16 * ld + (col >> 4) * 256 + 16 * (col & 15) + (row & 15);
+  return (size_t)(row >> 4) * 16 * ld + (col >> 4) * 256 + 16 * (row & 15) + (col & 15);
 }
 
 struct TNWArgs {

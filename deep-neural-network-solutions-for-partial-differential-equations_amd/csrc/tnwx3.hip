@@ -162,32 +162,29 @@ __device__ __forceinline__ void x3_products(floatx4 (&acc)[NB][NB], const TNWPro
   }
 }
 
-// The same pipeline over operands in column tiles (the fused phase kernels'
-// stores, tnw.hpp op_off): a lane's rows 8q .. 8q + 7 of column 16 m + i are
-// 32 contiguous bytes in 16-row tile 2 g + (q >> 1), so a block is two 16-byte
-// loads instead of eight dword loads.  Per operand the lane's byte offset of
-// step g is g 32 ld4 + lo, lo = 4 ((q >> 1) 16 ld + 16 i + 8 (q & 1)), block m
-// at + 1024 m.  TB1: B1 in column tiles too (block problems); the x-stack
-// problems' B1 is xin, row-major (the old loads, chosen per step by a
+// The same pipeline over operands in block tiles (the fused phase kernels'
+// stores, tnw.hpp op_off): a 16 x 16 block of a 16-row tile is 1 KiB,
+// row-major inside, so a lane's rows 8q .. 8q + 7 of column 16 m + i are eight
+// dword loads 64 bytes apart, each instruction reading 64 contiguous bytes per
+// row as the row-major loads do.  Per operand the lane's byte offset of step g
+// is g 32 ld4 + lo, lo = 4 ((q >> 1) 16 ld + 128 (q & 1) + i), block m at
+// + 1024 m.  TB1: B1 in block tiles too (block problems); the x-stack
+// problems' B1 is xin, row-major (the row-major loads, chosen per step by a
 // wave-uniform branch).
-__device__ __forceinline__ floatx4 bload4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
-  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
-}
 __device__ __forceinline__ void tload_block(float (&r)[8], __amdgpu_buffer_rsrc_t rs, unsigned voff) {
-  const floatx4 a = bload4(rs, voff, 0u), b = bload4(rs, voff, 16u);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    r[j] = a[j];
-    r[4 + j] = b[j];
-  }
+  for (int j = 0; j < 8; ++j) r[j] = bload1(rs, voff, 64u * j);
 }
+// (block-major: consecutive loads share their 128-byte lines, two rows each)
 template <int NB>
 __device__ __forceinline__ void tload_cols(float (&r)[NB][8], __amdgpu_buffer_rsrc_t rs, unsigned voff) {
 #pragma unroll
-  for (int m = 0; m < NB; ++m) tload_block(r[m], rs, voff + 1024u * m);
+  for (int m = 0; m < NB; ++m)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[m][j] = bload1(rs, voff + 1024u * m, 64u * j);
 }
 __device__ __forceinline__ unsigned tile_lo(int ld, int i, int q) {
-  return 4u * ((unsigned)(q >> 1) * 16u * (unsigned)ld + 16u * (unsigned)i + 8u * (unsigned)(q & 1));
+  return 4u * ((unsigned)(q >> 1) * 16u * (unsigned)ld + 128u * (unsigned)(q & 1) + (unsigned)i);
 }
 template <int NB, bool TB1>
 __device__ __forceinline__ void x3_products_tile(floatx4 (&acc)[NB][NB], const TNWProb& pr, int g0, int g1, int i,
@@ -250,7 +247,7 @@ __device__ __forceinline__ void x3_products_tile(floatx4 (&acc)[NB][NB], const T
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
         __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // VALU
       }
-      if (m + 1 < NB) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);   // VMEM read
+      if (m + 1 < NB) __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);   // VMEM read
       __builtin_amdgcn_sched_barrier(0);
       sa = san;
     }
