@@ -34,15 +34,6 @@
 #ifndef DBSDE_DEFER_PF
 #define DBSDE_DEFER_PF 1
 #endif
-// the fused phase kernels write the weight-gradient operands in block tiles
-// (phase.hpp bstore_stream) when the wave-owned tiles read them: the phase
-// section gains 30-38 us (1 KiB contiguous stores), but the weight-gradient
-// kernel reading the same bytes from block tiles loses 35-58 us with the same
-// instruction stream (column tiles, block tiles, block-major orders:
-// profiles/r6_ab_phase.txt 5), so the default stays row-major
-#ifndef DBSDE_OPTILE
-#define DBSDE_OPTILE 0
-#endif
 // device-mode diagonal rollout with the draws spread over the time steps
 // (rollout_steps_kernel, 1) or one thread per (path, column group) for all
 // steps (rollout4_kernel, 0).  The prefetched rollout is off the step's
@@ -1467,39 +1458,31 @@ int prep_weights(dbsde_ctx* c, const float* params) {
 // (alpha_j^T h_{j-1} + delta_j^T hdot_{j-1}); plus the output-layer column sums.
 // Slices [s0, s0 + sn) (sn < 0: all), on stream st without profiling records
 // (st == nullptr: the context stream, profiled).
-// tile: the operands H, Delta, Hdot, Alpha, zbar were written in tile order
-// (the fused phase kernels, FusedArgs.optile); the chain path writes them
-// row-major.  A tile-order level starting at column col begins 16 col floats
-// into its buffer (tnw.hpp op_off); xin is always row-major.
-int launch_tnw(dbsde_ctx* c, int R, int Rp, bool tile, int s0 = 0, int sn = -1, hipStream_t st = nullptr) {
+int launch_tnw(dbsde_ctx* c, int R, int Rp, int s0 = 0, int sn = -1, hipStream_t st = nullptr) {
   const int K = c->K, S = c->Stot, T = c->Dp;
-  const int cm = tile ? 16 : 1;   // column offset -> element offset of a level's first column
   TNWArgs a;
   memset(&a, 0, sizeof(a));
   for (int j = 0; j <= K; ++j) {
     TNWProb& p = a.prob[j];
-    p.A1 = c->Alpha + cm * c->col[j];
+    p.A1 = c->Alpha + c->col[j];
     p.lda1 = S;
     p.B1 = c->xin;
     p.ldb1 = c->Dp;
-    p.A2 = c->Delta + cm * c->col[j];
+    p.A2 = c->Delta + c->col[j];
     p.lda2 = S;
     p.B2 = c->zbar;
     p.ldb2 = c->Dp;
-    p.ta = p.tb2 = tile;
-    p.tb1 = 0;
   }
   for (int j = 1; j <= K; ++j) {
     TNWProb& p = a.prob[K + j];
-    p.A1 = c->Alpha + cm * c->col[j];
+    p.A1 = c->Alpha + c->col[j];
     p.lda1 = S;
-    p.B1 = c->H + cm * c->col[j - 1];
+    p.B1 = c->H + c->col[j - 1];
     p.ldb1 = S;
-    p.A2 = c->Delta + cm * c->col[j];
+    p.A2 = c->Delta + c->col[j];
     p.lda2 = S;
-    p.B2 = c->Hdot + cm * c->col[j - 1];
+    p.B2 = c->Hdot + c->col[j - 1];
     p.ldb2 = S;
-    p.ta = p.tb1 = p.tb2 = tile;
   }
   a.P = c->tnw_P;
   a.S = c->tnw_S;
@@ -1508,10 +1491,9 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp, bool tile, int s0 = 0, int sn = -1, 
   a.nchunk = Rp / 16;
   a.slab = c->slabW;
   a.ubar = c->ubar;
-  a.Hk = c->H + cm * c->col[K];
-  a.Hdk = c->Hdot + cm * c->col[K];
+  a.Hk = c->H + c->col[K];
+  a.Hdk = c->Hdot + c->col[K];
   a.ldh = S;
-  a.tile_h = tile;
   a.R = R;
   if (Rp % 16 != 0 || c->Wp[K] != T || a.S % 8 != 0 || a.P != 2 * K + 2 || a.P % 4 != 0 || a.sn % 8 != 0 ||
       a.s0 < 0 || a.s0 + a.sn > a.S)
@@ -1738,8 +1720,6 @@ FusedArgs fused_args(dbsde_ctx* c, int R, int Rp, int N1, bool q3) {
   a.zbar = c->zbar;
   a.ubar = c->ubar;
   a.u16 = c->tnw ? nullptr : c->u16;
-  // the weight-gradient operands in tile order for the wave-owned tiles
-  a.optile = (c->tnw && DBSDE_OPTILE) ? 1 : 0;
   a.loss_part = c->loss_part;
   a.Hdot = c->Hdot;
   a.Alpha = c->Alpha;
@@ -2149,7 +2129,7 @@ int backward_tail(dbsde_ctx* c, const float* params, int R, int Rp, int fv, floa
   }
   // ---- parameter gradients
   if (c->tnw) {
-    if (!tnw_piped && (rc = launch_tnw(c, R, Rp, fv >= 0 && DBSDE_OPTILE))) return rc;
+    if (!tnw_piped && (rc = launch_tnw(c, R, Rp))) return rc;
     if ((rc = finalize_grads(c, params, grad, loss_part, nloss_parts, loss_dst, fo))) return rc;
   } else {
   if (!tn_piped) {
@@ -2319,7 +2299,7 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         const int tiles = i + 1 < nch ? cu[i] * utile : Rp / WR - t0;
         kFused[fv].A<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
         kFused[fv].C<<<tiles, 64 * P3_WAVES, 0, st>>>(fc);
-        if (tnw_piped && (rc = launch_tnw(c, R, Rp, fa.optile != 0, sb[i], sb[i + 1] - sb[i], st))) return rc;
+        if (tnw_piped && (rc = launch_tnw(c, R, Rp, sb[i], sb[i + 1] - sb[i], st))) return rc;
         if (tn_piped && (rc = tn_launch_splits(c, R, tn_a, tn_g, i == 0 ? 0 : tn_s0,
                                                i == 0 ? tn_s0 : tn_g.S_ - tn_s0, st)))
           return rc;

@@ -47,7 +47,6 @@ struct FusedArgs {
   float* u16;               // [Rp, 16] col 0 = ubar (split-K weight-gradient path) or null
   double* loss_part;        // [Rp / 64] per-workgroup loss sums
   float *Hdot, *Alpha;
-  int optile;               // H, Delta, Hdot, Alpha, zbar in tile order (phase.hpp bstore_stream)
   float* Adot;              // phase2 ADOT kernels: adot_j between the tangent and the reverse (tile order)
   // fragment images of the stage sequence of each pass (phase.hpp)
   // (fp32 images: two pieces per stage; split-bf16 images: one piece per

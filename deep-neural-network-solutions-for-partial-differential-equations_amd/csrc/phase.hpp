@@ -42,9 +42,13 @@ namespace dbsde {
 // Alpha, zbar), bit 2 no Abuf / G stores (phase C still loads them), bit 3 no
 // wait for the piece DMA, bit 4 no operand splits (one perm instead of the
 // hi / mid / lo split), bit 5 no LDS fragment reads (the piece's first
-// fragment reused); the operand stores of bstore_stream: bit 6 cached instead
-// of non-temporal, bit 7 tile order, bit 11 into LDS instead, bit 12 the even
-// blocks only.
+// fragment reused); the weight-gradient operand stores: bit 6 cached instead
+// of non-temporal, bit 7 in tile order (1 KB contiguous per instruction),
+// bit 8 column-major 16 x 16 blocks (4 dword stores per block), bits 9 / 10
+// folded into the first 8192 / 512 rows (cache-resident footprints), bit 11
+// into LDS instead, bit 12 the even blocks only.  The tiled layouts as real
+// variants (phase kernels write, weight-gradient kernel reads) measured slower
+// per step: profiles/r6_ab_phase.txt 5.
 #ifndef DBSDE_AB_PHASE
 #define DBSDE_AB_PHASE 0
 #endif
@@ -95,38 +99,32 @@ __device__ __forceinline__ void fload(Mat<TT>& m, const float* base, int ld, int
 // both phases (H, Delta, Hdot, Alpha, zbar): no L2 allocate, so Abuf / G / zfull,
 // which phase C re-reads shortly after phase A wrote them, keep the cache
 // (measured -13 us on the two phases, profiles/r2_ab_ntstore.txt)
-// tile = true: the "block tile" layout instead (FusedArgs.optile; the
-// wave-owned weight-gradient kernel reads either, tnw.hpp op_off): in each
-// 16-row tile, every 16 x 16 block is 1 KiB contiguous, row-major inside
-// (element (r, c) at 16 r + c).  A lane's float4 (row cl, columns 4q .. 4q + 3)
-// lands at 16 cl + 4 q, so one store instruction writes one whole block --
-// 1 KiB contiguous instead of 64 bytes in each of 16 rows -- and the
-// weight-gradient kernel still reads 64 contiguous bytes per row per
-// instruction.  The phase kernels' stores are issue-bound: the 7.6 KB per row
-// of these operands cost the phase section 0.12 ms against 0.06 ms written to
-// LDS instead (profiles/r6_ab_phase.txt).
 template <int TT>
-__device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int ld, int row0, int col0,
-                                              bool tile = false) {
+__device__ __forceinline__ void bstore_stream(const Mat<TT>& m, float* base, int ld, int row0, int col0) {
   if constexpr (DBSDE_AB_PHASE & 2) return;
   const int lane = threadIdx.x & 63;
-  if constexpr (DBSDE_AB_PHASE & 2048) {   // (ablation: into LDS instead, over the ring's first KB)
-#pragma unroll
-    for (int t = 0; t < TT; ++t) asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(16 * lane)), "v"(m.v[t]));
-    return;
-  }
-  if (tile) {
-    float* p = base + (size_t)row0 * ld + col0 * 16 + 16 * (lane & 15) + 4 * (lane >> 4);
-#pragma unroll
-    for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 256 * t));
-    return;
-  }
-  if constexpr (DBSDE_AB_PHASE & 128) {   // (ablation: fstore's tile order, no transpose)
+  if constexpr (DBSDE_AB_PHASE & 128) {   // (ablation: tile order, 1 KB contiguous per instruction)
     float* p = base + (size_t)row0 * ld + col0 * 16 + 4 * lane;
 #pragma unroll
     for (int t = 0; t < TT; ++t) __builtin_nontemporal_store(m.v[t], (floatx4*)(p + 256 * t));
     return;
   }
+  if constexpr (DBSDE_AB_PHASE & 256) {   // (ablation: column-major 16x16 blocks, 4 dword stores)
+    const int cl = lane & 15, q = lane >> 4;
+    float* p = base + (size_t)row0 * ld + col0 * 16 + 64 * q + cl;
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) __builtin_nontemporal_store(m.v[t][r], p + 256 * t + 16 * r);
+    return;
+  }
+  if constexpr (DBSDE_AB_PHASE & 2048) {   // (ablation: into LDS instead, over the ring's first KB)
+#pragma unroll
+    for (int t = 0; t < TT; ++t) asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(16 * lane)), "v"(m.v[t]));
+    return;
+  }
+  if constexpr (DBSDE_AB_PHASE & 512) row0 &= 8191;   // (ablation: a 60 MB footprint, MALL-resident)
+  if constexpr (DBSDE_AB_PHASE & 1024) row0 &= 511;   // (ablation: a 4 MB footprint, L2-resident)
   float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
@@ -634,7 +632,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
   SFor<1, K + 1>::run([&](auto jc) __attribute__((always_inline)) {
     constexpr int j = decltype(jc)::value;
     zero(acc);
-    stage_mm<X3, T, T, T, T, PFA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd, p.optile); });
+    stage_mm<X3, T, T, T, T, PFA>(acc, h, sg, lane, [&]() __attribute__((always_inline)) { bstore_stream(h, p.H, S, row0, (j - 1) * Wd); });
     if constexpr (HV) stage_mm<X3, T, TD, 0, 0, PFA>(acc, x, sg, lane, NoOp{});
 #pragma unroll
     for (int o = 0; o < T; ++o) {
@@ -675,7 +673,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
     }
     if (q == 0) p.u[row0 + cl] = uv;
   }
-  bstore_stream(h, p.H, S, row0, K * Wd, p.optile);
+  bstore_stream(h, p.H, S, row0, K * Wd);
   // input gradient: g_{K+1} = w_out, delta_K = w_out act'(a_K)
   Mat<T> g, dl;
 #pragma unroll
@@ -695,7 +693,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
     constexpr int j = K - decltype(ic)::value;
     auto prev = [&]() __attribute__((always_inline)) {   // (g_j, delta_j) of the previous step
       if constexpr (j < K) fstore(g, p.G, S, row0, j * Wd);
-      bstore_stream(dl, p.Delta, S, row0, j * Wd, p.optile);
+      bstore_stream(dl, p.Delta, S, row0, j * Wd);
       if constexpr (RECOMP) fload(av, p.Abuf, S, row0, (j - 1) * Wd);
     };
     Mat<T> gn;
@@ -718,7 +716,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseA_kernel
   });
   stage_mm<X3, TD, T, 0, 2 * T + TD, PFA>(z, dl, sg, lane, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
     fstore(g, p.G, S, row0, 0);
-    bstore_stream(dl, p.Delta, S, row0, 0, p.optile);
+    bstore_stream(dl, p.Delta, S, row0, 0);
     bload(x, p.xin, p.Dp, row0, 0);
   });
   if (p.u_clamp) {
@@ -820,7 +818,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
                           : 0.f;
       }
   }
-  bstore_stream(zb, p.zbar, p.Dp, row0, 0, p.optile);
+  bstore_stream(zb, p.zbar, p.Dp, row0, 0);
   tz += __shfl_xor(tz, 16);
   tz += __shfl_xor(tz, 32);
   {
@@ -871,7 +869,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
     constexpr int j = decltype(jc)::value;
     if constexpr (!XFIRST) zero(ad[j]);
     stage_mm<X3, T, T, 0, 2 * T, PFC_T>(ad[j], hd, sg, lane, [&]() __attribute__((always_inline)) {
-      bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd, p.optile);
+      bstore_stream(hd, p.Hdot, S, row0, (j - 1) * Wd);
       fload(av, p.Abuf, S, row0, j * Wd);
     });
     if constexpr (HV && !XFIRST) stage_mm<X3, T, TD, 0, 0, PFC_T>(ad[j], zb, sg, lane, NoOp{});
@@ -880,7 +878,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) hd.v[o][rr] = act_1<ACT>(av.v[o][rr]) * ad[j].v[o][rr] + p.rho * hd.v[o][rr];
   });
-  bstore_stream(hd, p.Hdot, S, row0, K * Wd, p.optile);
+  bstore_stream(hd, p.Hdot, S, row0, K * Wd);
   // reverse: p_{K+1} = ubar w_out ; alpha_K = w_out (ubar act'(a_K) + adot_K act''(a_K))
   Mat<T> pv, al;
   {
@@ -902,7 +900,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
     Mat<T> acc, gg;
     zero(acc);
     stage_mm<X3, T, T, 0, 3 * T, PFC_R>(acc, al, sg, lane, [&]() __attribute__((always_inline)) {   // alpha_j B_j
-      bstore_stream(al, p.Alpha, S, row0, j * Wd, p.optile);
+      bstore_stream(al, p.Alpha, S, row0, j * Wd);
       fload(av, p.Abuf, S, row0, (j - 1) * Wd);
       fload(gg, p.G, S, row0, (j - 1) * Wd);
     });
@@ -917,7 +915,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2 * P3_WAVES / 4) phaseC_kernel
         al.v[o][rr] = pp * d1 + gg.v[o][rr] * ad[j - 1].v[o][rr] * d2;
       }
   });
-  bstore_stream(al, p.Alpha, S, row0, 0, p.optile);
+  bstore_stream(al, p.Alpha, S, row0, 0);
 }
 
 }  // namespace dbsde

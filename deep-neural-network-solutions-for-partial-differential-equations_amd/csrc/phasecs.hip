@@ -48,16 +48,8 @@ __device__ __forceinline__ void fload_n(Mat<2>& m, const float* base, int ld, in
   m.v[0] = *(const floatx4*)p;
   m.v[1] = *(const floatx4*)(p + (n > 1 ? 256 : 0));
 }
-// (tile: phase.hpp bstore_stream's block tiles, FusedArgs.optile)
-__device__ __forceinline__ void bstore_stream_n(const Mat<2>& m, float* base, int ld, int row0, int col0, int n,
-                                                bool tile) {
+__device__ __forceinline__ void bstore_stream_n(const Mat<2>& m, float* base, int ld, int row0, int col0, int n) {
   const int lane = threadIdx.x & 63;
-  if (tile) {   // (phase.hpp bstore_stream: block tiles)
-    float* p = base + (size_t)row0 * ld + col0 * 16 + 16 * (lane & 15) + 4 * (lane >> 4);
-    __builtin_nontemporal_store(m.v[0], (floatx4*)p);
-    __builtin_nontemporal_store(pick(n > 1, m.v[1], m.v[0]), (floatx4*)(p + (n > 1 ? 256 : 0)));
-    return;
-  }
   float* p = base + (size_t)(row0 + (lane & 15)) * ld + col0 + 4 * (lane >> 4);
   __builtin_nontemporal_store(m.v[0], (floatx4*)p);
   __builtin_nontemporal_store(pick(n > 1, m.v[1], m.v[0]), (floatx4*)(p + (n > 1 ? 16 : 0)));
@@ -359,7 +351,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseAcs_kernel(FusedArgs p)
     constexpr int j = decltype(jc)::value;
     zero(acc);
     stage_cs<T, 1, 1, true>(acc, hf, sg, lane, w, xb, [&]() __attribute__((always_inline)) {
-      bstore_stream_n(ho, p.H, S, row0, (j - 1) * Wd + c0, w.n, p.optile);
+      bstore_stream_n(ho, p.H, S, row0, (j - 1) * Wd + c0, w.n);
     });
     if constexpr (HV) stage_cs<TD, 0, 0, false>(acc, x, sg, lane, w, xb, NoOp{});
     if constexpr (!HV) {
@@ -403,7 +395,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseAcs_kernel(FusedArgs p)
     }
     if (wave == 0 && q == 0) p.u[row0 + cl] = uv;
   }
-  bstore_stream_n(ho, p.H, S, row0, K * Wd + c0, w.n, p.optile);
+  bstore_stream_n(ho, p.H, S, row0, K * Wd + c0, w.n);
   // input gradient: g_{K+1} = w_out, delta_K = w_out act'(a_K)
   Mat<2> g, dl;
 #pragma unroll
@@ -423,7 +415,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseAcs_kernel(FusedArgs p)
     constexpr int j = K - decltype(ic)::value;
     auto prev = [&]() __attribute__((always_inline)) {   // (g_j, delta_j) of the previous step
       if constexpr (j < K) fstore_n(g, p.G, S, row0, j * Wd + c0, w.n);
-      bstore_stream_n(dl, p.Delta, S, row0, j * Wd + c0, w.n, p.optile);
+      bstore_stream_n(dl, p.Delta, S, row0, j * Wd + c0, w.n);
     };
     Mat<2> gn;
     zero(gn);
@@ -446,7 +438,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseAcs_kernel(FusedArgs p)
   });
   stage_cs<T, 0, 2, true>(z, df, sg, lane, w, xb, [&]() __attribute__((always_inline)) {   // Z += delta_0 W_in
     fstore_n(g, p.G, S, row0, c0, w.n);
-    bstore_stream_n(dl, p.Delta, S, row0, c0, w.n, p.optile);
+    bstore_stream_n(dl, p.Delta, S, row0, c0, w.n);
   });
   if (p.u_clamp) {
 #pragma unroll
@@ -561,7 +553,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseCcs_kernel(FusedArgs p)
   tz += __shfl_xor(tz, 16);
   tz += __shfl_xor(tz, 32);
   if (wave == 0) {
-    bstore_stream(zb, p.zbar, p.Dp, row0, 0, p.optile);
+    bstore_stream(zb, p.zbar, p.Dp, row0, 0);
     double lv = (rc.valid && q == 0) ? (double)(rc.res * rc.res + tz) : 0.0;
 #pragma unroll
     for (int s = 1; s < 16; s <<= 1) lv += __shfl_xor(lv, s);
@@ -596,7 +588,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseCcs_kernel(FusedArgs p)
     constexpr int j = decltype(jc)::value;
     if constexpr (!XFIRST) zero(ad[j]);
     stage_cs<T, 0, 2, true>(ad[j], hf, sg, lane, w, xb, [&]() __attribute__((always_inline)) {
-      bstore_stream_n(hdo, p.Hdot, S, row0, (j - 1) * Wd + c0, w.n, p.optile);
+      bstore_stream_n(hdo, p.Hdot, S, row0, (j - 1) * Wd + c0, w.n);
       fload_n(avo, p.Abuf, S, row0, j * Wd + c0, w.n);
     });
 #pragma unroll
@@ -605,7 +597,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseCcs_kernel(FusedArgs p)
       for (int rr = 0; rr < 4; ++rr) hdo.v[o][rr] = act_1<ACT>(avo.v[o][rr]) * ad[j].v[o][rr] + p.rho * hdo.v[o][rr];
     if constexpr (j < K) xput(hdo, xb, w, lane);
   });
-  bstore_stream_n(hdo, p.Hdot, S, row0, K * Wd + c0, w.n, p.optile);
+  bstore_stream_n(hdo, p.Hdot, S, row0, K * Wd + c0, w.n);
   // reverse: p_{K+1} = ubar w_out ; alpha_K = w_out (ubar act'(a_K) + adot_K act''(a_K))
   Mat<2> pv, al;
   {
@@ -629,7 +621,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseCcs_kernel(FusedArgs p)
     Mat<2> acc, gg;
     zero(acc);
     stage_cs<T, 0, 3, true>(acc, af, sg, lane, w, xb, [&]() __attribute__((always_inline)) {   // alpha_j B_j
-      bstore_stream_n(al, p.Alpha, S, row0, j * Wd + c0, w.n, p.optile);
+      bstore_stream_n(al, p.Alpha, S, row0, j * Wd + c0, w.n);
       fload_n(avo, p.Abuf, S, row0, (j - 1) * Wd + c0, w.n);
       fload_n(gg, p.G, S, row0, (j - 1) * Wd + c0, w.n);
     });
@@ -645,7 +637,7 @@ __global__ void __launch_bounds__(64 * P3_WAVES, 2) phaseCcs_kernel(FusedArgs p)
       }
     if constexpr (j > 1) xput(al, xb, w, lane);
   });
-  bstore_stream_n(al, p.Alpha, S, row0, c0, w.n, p.optile);
+  bstore_stream_n(al, p.Alpha, S, row0, c0, w.n);
 }
 
 #define DBSDE_PHASECS_DEFINE(T, TD, K, ACT, HV)                           \

@@ -14,17 +14,14 @@ struct TnwStage {
   float a[NB], b[NB];
 };
 
-// (ta / tb: the operands' layouts, tnw.hpp; wave-uniform)
 template <int NB>
-__device__ __forceinline__ void tnw_load(const float* A, int lda, bool ta, const float* B, int ldb, bool tb, int row,
-                                         int i, TnwStage<NB>& st) {
-  const float* a = A + (ta ? op_off<true>(row, i, lda) : op_off<false>(row, i, lda));
-  const float* b = B + (tb ? op_off<true>(row, i, ldb) : op_off<false>(row, i, ldb));
-  const int sa = ta ? 256 : 16, sb = tb ? 256 : 16;   // block strides
+__device__ __forceinline__ void tnw_load(const float* A, int lda, const float* B, int ldb, int row, int i,
+                                         TnwStage<NB>& st) {
+  const size_t r = (size_t)row;
 #pragma unroll
   for (int m = 0; m < NB; ++m) {
-    st.a[m] = a[sa * m];
-    st.b[m] = b[sb * m];
+    st.a[m] = A[r * lda + 16 * m + i];
+    st.b[m] = B[r * ldb + 16 * m + i];
   }
 }
 
@@ -42,24 +39,24 @@ __device__ __forceinline__ void tnw_mma(floatx4 (&acc)[NB][NB], const TnwStage<N
 // slice are clamped to its last step and never used), so the accumulators
 // stay in place and the waitcnts only cover the stage being consumed.
 template <int NB>
-__device__ __forceinline__ void tnw_product(floatx4 (&acc)[NB][NB], const float* A, int lda, bool ta, const float* B,
-                                            int ldb, bool tb, int g0, int g1, int i, int kq) {
+__device__ __forceinline__ void tnw_product(floatx4 (&acc)[NB][NB], const float* A, int lda, const float* B, int ldb,
+                                            int g0, int g1, int i, int kq) {
   TnwStage<NB> q0, q1, q2;
   const int gl = g1 - 1;
   // three-stage ring with a 3-step body (fixed rotation), then a 0-2 step tail
-  tnw_load<NB>(A, lda, ta, B, ldb, tb, 4 * g0 + kq, i, q0);
-  tnw_load<NB>(A, lda, ta, B, ldb, tb, 4 * (g0 + 1) + kq, i, q1);
+  tnw_load<NB>(A, lda, B, ldb, 4 * g0 + kq, i, q0);
+  tnw_load<NB>(A, lda, B, ldb, 4 * (g0 + 1) + kq, i, q1);
   int g = g0;
   for (; g + 3 <= g1; g += 3) {
-    tnw_load<NB>(A, lda, ta, B, ldb, tb, 4 * (g + 2) + kq, i, q2);
+    tnw_load<NB>(A, lda, B, ldb, 4 * (g + 2) + kq, i, q2);
     __builtin_amdgcn_sched_barrier(0);
     tnw_mma<NB>(acc, q0);
     __builtin_amdgcn_sched_barrier(0);
-    tnw_load<NB>(A, lda, ta, B, ldb, tb, 4 * min(g + 3, gl) + kq, i, q0);
+    tnw_load<NB>(A, lda, B, ldb, 4 * min(g + 3, gl) + kq, i, q0);
     __builtin_amdgcn_sched_barrier(0);
     tnw_mma<NB>(acc, q1);
     __builtin_amdgcn_sched_barrier(0);
-    tnw_load<NB>(A, lda, ta, B, ldb, tb, 4 * min(g + 4, gl) + kq, i, q1);
+    tnw_load<NB>(A, lda, B, ldb, 4 * min(g + 4, gl) + kq, i, q1);
     __builtin_amdgcn_sched_barrier(0);
     tnw_mma<NB>(acc, q2);
     __builtin_amdgcn_sched_barrier(0);
@@ -96,8 +93,8 @@ __global__ void __launch_bounds__(256, 1) tnw_kernel(TNWArgs a) {
     return;
   }
   if (g1 > g0) {
-    tnw_product<NB>(acc, pr.A1, pr.lda1, pr.ta, pr.B1, pr.ldb1, pr.tb1, g0, g1, i, kq);
-    tnw_product<NB>(acc, pr.A2, pr.lda2, pr.ta, pr.B2, pr.ldb2, pr.tb2, g0, g1, i, kq);
+    tnw_product<NB>(acc, pr.A1, pr.lda1, pr.B1, pr.ldb1, g0, g1, i, kq);
+    tnw_product<NB>(acc, pr.A2, pr.lda2, pr.B2, pr.ldb2, g0, g1, i, kq);
   }
 #pragma unroll
   for (int m = 0; m < NB; ++m)

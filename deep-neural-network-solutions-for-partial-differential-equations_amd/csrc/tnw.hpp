@@ -32,21 +32,7 @@ struct TNWProb {
   const float* A2;
   const float* B2;
   int lda1, ldb1, lda2, ldb2;
-  // operand layouts: 0 row-major [rows, ld]; 1 block tiles (phase.hpp
-  // bstore_stream: each 16 x 16 block of a 16-row tile is 256 contiguous
-  // floats, row-major inside, element (row, col) at 16 row + col) -- the fused
-  // phase kernels write the weight-gradient operands that way.  A1 and A2
-  // share ta.
-  int ta, tb1, tb2;
 };
-
-// element (row, col) of an operand of row stride ld in either layout (a
-// compile-time layout: the kernels branch once per wave, never per load)
-template <bool TILE>
-__device__ __forceinline__ size_t op_off(int row, int col, int ld) {
-  if constexpr (!TILE) return (size_t)row * ld + col;
-  return (size_t)(row >> 4) * 16 * ld + (col >> 4) * 256 + 16 * (row & 15) + (col & 15);
-}
 
 struct TNWArgs {
   TNWProb prob[TNW_PMAX];
@@ -60,7 +46,6 @@ struct TNWArgs {
   const float* Hk;
   const float* Hdk;
   int ldh;        // row stride of Hk/Hdk
-  int tile_h;     // Hk / Hdk in tile order (TNWProb)
   int R;          // valid rows
 };
 
@@ -78,8 +63,8 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // Output layer [w_out | b_out]: sum_r ubar_r h_r + hdot_r (and sum_r ubar_r)
 // as a one-block-row product whose A operand [ubar | 1 | 0 ...] is formed in
 // registers; row 0 of the tile is w_out, element (1, 0) is b_out.
-template <int NB, bool TILE>
-__device__ __forceinline__ void tnw_output_t(const TNWArgs& a, int g0, int g1, int i, int kq, float* out) {
+template <int NB>
+__device__ __forceinline__ void tnw_output(const TNWArgs& a, int g0, int g1, int i, int kq, float* out) {
   floatx4 acc[NB];
 #pragma unroll
   for (int n = 0; n < NB; ++n) acc[n] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -90,15 +75,13 @@ __device__ __forceinline__ void tnw_output_t(const TNWArgs& a, int g0, int g1, i
     const float ub = a.ubar[row];
     const float a1 = i == 0 ? ub : 0.f;
     const float a2 = (i == 0 && row < a.R) ? 1.f : 0.f;
-    const size_t o = op_off<TILE>(row, i, a.ldh);
-    const float* h = a.Hk + o;
-    const float* hd = a.Hdk + o;
-    constexpr int BS = TILE ? 256 : 16;   // block stride
+    const float* h = a.Hk + (size_t)row * a.ldh + i;
+    const float* hd = a.Hdk + (size_t)row * a.ldh + i;
     float b1[NB], b2[NB];
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
-      b1[n] = h[BS * n];
-      b2[n] = hd[BS * n];
+      b1[n] = h[16 * n];
+      b2[n] = hd[16 * n];
     }
 #pragma unroll
     for (int n = 0; n < NB; ++n) {
@@ -115,13 +98,6 @@ __device__ __forceinline__ void tnw_output_t(const TNWArgs& a, int g0, int g1, i
   // b_out partial: lanes 0, 16, 32, 48 hold the sums of their k rows
   const float b = (__shfl(bs, 0) + __shfl(bs, 16)) + (__shfl(bs, 32) + __shfl(bs, 48));
   if ((threadIdx.x & 63) == 0) out[T] = b;
-}
-template <int NB>
-__device__ __forceinline__ void tnw_output(const TNWArgs& a, int g0, int g1, int i, int kq, float* out) {
-  if (a.tile_h)
-    tnw_output_t<NB, true>(a, g0, g1, i, kq, out);
-  else
-    tnw_output_t<NB, false>(a, g0, g1, i, kq, out);
 }
 
 

@@ -18,9 +18,6 @@
 // MFMAs of the previous block (x3_products).
 #include "tnw.hpp"
 
-#ifndef DBSDE_TNW_ONLY
-#define DBSDE_TNW_ONLY 0
-#endif
 #ifndef DBSDE_TNW_INTERLEAVE
 #define DBSDE_TNW_INTERLEAVE 1
 #endif
@@ -162,98 +159,6 @@ __device__ __forceinline__ void x3_products(floatx4 (&acc)[NB][NB], const TNWPro
   }
 }
 
-// The same pipeline over operands in block tiles (the fused phase kernels'
-// stores, tnw.hpp op_off): a 16 x 16 block of a 16-row tile is 1 KiB,
-// row-major inside, so a lane's rows 8q .. 8q + 7 of column 16 m + i are eight
-// dword loads 64 bytes apart, each instruction reading 64 contiguous bytes per
-// row as the row-major loads do.  Per operand the lane's byte offset of step g
-// is g 32 ld4 + lo, lo = 4 ((q >> 1) 16 ld + 128 (q & 1) + i), block m at
-// + 1024 m.  TB1: B1 in block tiles too (block problems); the x-stack
-// problems' B1 is xin, row-major (the row-major loads, chosen per step by a
-// wave-uniform branch).
-__device__ __forceinline__ void tload_block(float (&r)[8], __amdgpu_buffer_rsrc_t rs, unsigned voff) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = bload1(rs, voff, 64u * j);
-}
-// (block-major: consecutive loads share their 128-byte lines, two rows each)
-template <int NB>
-__device__ __forceinline__ void tload_cols(float (&r)[NB][8], __amdgpu_buffer_rsrc_t rs, unsigned voff) {
-#pragma unroll
-  for (int m = 0; m < NB; ++m)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[m][j] = bload1(rs, voff + 1024u * m, 64u * j);
-}
-__device__ __forceinline__ unsigned tile_lo(int ld, int i, int q) {
-  return 4u * ((unsigned)(q >> 1) * 16u * (unsigned)ld + 128u * (unsigned)(q & 1) + (unsigned)i);
-}
-template <int NB, bool TB1>
-__device__ __forceinline__ void x3_products_tile(floatx4 (&acc)[NB][NB], const TNWProb& pr, int g0, int g1, int i,
-                                                 int q) {
-  const int n = g1 - g0, last = 2 * n - 1;
-  const __amdgpu_buffer_rsrc_t rA1 = rsrc_of(pr.A1), rA2 = rsrc_of(pr.A2), rB1 = rsrc_of(pr.B1), rB2 = rsrc_of(pr.B2);
-  const unsigned gsa1 = 128u * pr.lda1, gsa2 = 128u * pr.lda2, gsb1 = 128u * pr.ldb1, gsb2 = 128u * pr.ldb2;
-  const unsigned loa1 = tile_lo(pr.lda1, i, q), loa2 = tile_lo(pr.lda2, i, q), lob2 = tile_lo(pr.ldb2, i, q);
-  const unsigned ldb1 = 4u * pr.ldb1;   // (row-major B1)
-  const unsigned lob1 = TB1 ? tile_lo(pr.ldb1, i, q) : 8u * q * ldb1 + 4u * i;
-  float ra[NB][8], rb[NB][8];
-  if constexpr (TB1)
-    tload_cols<NB>(rb, rB1, g0 * gsb1 + lob1);
-  else
-    load_cols<NB>(rb, rB1, g0 * gsb1 + lob1, ldb1);
-  tload_cols<NB>(ra, rA1, g0 * gsa1 + loa1);   // every A block of the first step
-  Split3 sa = split8(ra[0]);   // A block 0 of the step (the last region splits the next step's)
-  for (int k = 0; k <= last; ++k) {
-    // the next step (clamped prefetch, unused past the end): product and row
-    const int kn = min(k + 1, last), second = kn >= n;
-    const __amdgpu_buffer_rsrc_t rA = second ? rA2 : rA1, rB = second ? rB2 : rB1;
-    const unsigned gn = (unsigned)(g0 + (second ? kn - n : kn));
-    const unsigned voa = gn * (second ? gsa2 : gsa1) + (second ? loa2 : loa1);
-    const unsigned vob = gn * (second ? gsb2 : gsb1) + (second ? lob2 : lob1);
-    Split3 sb[NB];
-#pragma unroll
-    for (int n = 0; n < NB; ++n) sb[n] = split8(rb[n]);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (TB1) {
-      tload_cols<NB>(rb, rB, vob);
-    } else {
-      if (second)
-        tload_cols<NB>(rb, rB, vob);
-      else
-        load_cols<NB>(rb, rB, vob, ldb1);
-    }
-    tload_block(ra[0], rA, voa);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int m = 0; m < NB; ++m) {
-      // region m splits A block m + 1 of this step, the last region block 0 of
-      // the next step (loaded at this step's top)
-      const Split3 san = split8(ra[m + 1 < NB ? m + 1 : 0]);
-      if (m + 1 < NB) tload_block(ra[m + 1], rA, voa + 1024u * (m + 1));
-      // product-major (x3_products)
-#pragma unroll
-      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.l, sb[n].h, acc[m][n]);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.h, sb[n].l, acc[m][n]);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.m, sb[n].m, acc[m][n]);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.m, sb[n].h, acc[m][n]);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.h, sb[n].m, acc[m][n]);
-#pragma unroll
-      for (int n = 0; n < NB; ++n) acc[m][n] = mfma_bf(sa.h, sb[n].h, acc[m][n]);
-#pragma unroll
-      for (int k = 0; k < 6 * NB; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);   // VALU
-      }
-      if (m + 1 < NB) __builtin_amdgcn_sched_group_barrier(0x020, 8, 0);   // VMEM read
-      __builtin_amdgcn_sched_barrier(0);
-      sa = san;
-    }
-  }
-}
-
 // the grid and problem / slice mapping of tnw_kernel (tnw.hip); slices are
 // whole 32-row steps
 template <int NB>
@@ -279,19 +184,7 @@ __global__ void __launch_bounds__(256, 1) tnw_x3_kernel(TNWArgs a) {
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
   if (c1 > c0) {
-    // (wave-uniform: the problem's operand layouts, tnw.hpp)
-#if DBSDE_TNW_ONLY == 1   // (A/B: the row-major pipeline only)
     x3_products<NB>(acc, pr, c0, c1, i, q);
-#elif DBSDE_TNW_ONLY == 2   // (A/B: the column-tile pipeline only; x-stack results wrong)
-    x3_products_tile<NB, true>(acc, pr, c0, c1, i, q);
-#else
-    if (!pr.ta)
-      x3_products<NB>(acc, pr, c0, c1, i, q);
-    else if (!pr.tb1)
-      x3_products_tile<NB, false>(acc, pr, c0, c1, i, q);   // x-stack: x row-major, zbar in tiles
-    else
-      x3_products_tile<NB, true>(acc, pr, c0, c1, i, q);
-#endif
   }
 #pragma unroll
   for (int m = 0; m < NB; ++m)
