@@ -46,7 +46,7 @@ PEAK_X3_TFLOPS = PEAK_BF16_DENSE_TFLOPS / 6.0
 X3_RECORDS = {1: ("fused_phases_pipelined", "fused_fwd_inputgrad", "fused_tangent_reverse"), 2: ("tn_weight_grad",),
               4: ("gemm_",)}
 PEAK_HBM_GBS = 8000.0
-PROFILE_ROUND = "r5"          # profiles/<round>_pmc_* counter collections of the current build
+PROFILE_ROUND = "r6"          # profiles/<round>_pmc_* counter collections of the current build
 # rocprof symbol of each profiled launch class (EPI ids from csrc/kernels.hpp)
 KERNEL_SYMBOL = {
     "gemm_xstack_fwd": "chain_gemm_kernel<7, 0>", "gemm_block_fwd": "chain_gemm_kernel<7, 1>",

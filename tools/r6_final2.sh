@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-6 final pass 2 (final build): kernel stats at the north star and at
+# M = 128, clock probe, the default bench line, the driver's window, the
+# other workloads and the strong-scaling shapes.
+export TMPDIR=/tmp
+out=gpurun_out/r6f
+mkdir -p $out
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  [ $rc -eq 0 ] || { tail -20 "$out/$name.log"; exit $rc; }
+}
+B="bench.py --no-cpu-baseline --no-parity"
+step stats_bsb 300 rocprofv3 --kernel-trace --stats -d $out/stats_bsb -o run --output-format csv -- python $B --steps 20 --warmup 5
+step stats_m128 300 rocprofv3 --kernel-trace --stats -d $out/stats_m128 -o run --output-format csv -- python $B --steps 20 --warmup 5 --paths-per-gpu 128
+step clocks 180 python tools/clock_probe.py --steps 100 --out $out/clocks.json
+step bench 600 python bench.py
+for i in 1 2 3; do step driver_$i 200 python $B --gpus 1 --steps 20 --warmup 5; done
+step bench_100_50 200 python $B --steps 100 --warmup 50
+for w in oned basket hjb heston; do step wl_$w 300 python $B --workload $w --steps 50 --warmup 10; done
+for m in 128 256 512; do step strong_$m 200 python $B --paths-per-gpu $m --steps 100 --warmup 10; done
+echo done
