@@ -1051,7 +1051,8 @@ int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
     const int nthr = ra.M * ra.nb;
     RUN(c, name, 0.0, bytes, rollout_heston_kernel<<<(nthr + 255) / 256, 256, 0, s>>>(ra));
   } else if (c->Lt && !ra.W) {
-    if (ra.ldx > CP_SROW) return fail(c, DBSDE_EINVAL, "internal: correlated rollout row staging");
+    if (ra.ldx > cp_srow((ra.nb + 15) / 16) || ra.ldx % 4 != 0)
+      return fail(c, DBSDE_EINVAL, "internal: correlated rollout row staging");
     RUN(c, name, 2.0 * steps * ra.nb * ra.nb / 2, bytes,
         launch_corr(ra, s));
   } else if (DBSDE_RS && ra.out == PATH_ROLLOUT && !ra.W && ra.ldx % 4 == 0) {

@@ -369,26 +369,41 @@ __global__ void __launch_bounds__(RS_THREADS) rollout_steps_kernel(RolloutArgs p
 // Philox draws of the next 4-step block (4 normals per (path, dim) call) are
 // made by all 512 threads into the other LDS buffer.  nb <= 128.
 // LDS: xi[buf][k][q][p][t] (dim 4 t + q of path p at step 4 blk + k), t
-// padded to 36 floats: the 16 paths of one q read 16-byte slots 36 floats
-// apart = distinct 4-bank groups (conflict-free ds_read_b128).
+// padded to TS = 28 (nb <= 112) or 36 floats: the 16 paths of one q read
+// 16-byte slots 28 / 36 floats apart = distinct 4-bank groups (conflict-free
+// ds_read_b128).
 // --------------------------------------------------------------------------
+// Timing-only ablations of the correlated rollout (results wrong by
+// construction, never built into the library): bit 0 no row stores, bit 1 no
+// draws after the first block, bit 2 no MFMA chain, bit 3 no per-step barrier.
+#ifndef DBSDE_AB_CORR
+#define DBSDE_AB_CORR 0
+#endif
 constexpr int CP_NBMAX = 128;
 constexpr int CP_PATHS = 16;
-constexpr int CP_TS = 36;
-constexpr int CP_BUF = 4 * 4 * CP_PATHS * CP_TS;   // floats per 4-step buffer
 constexpr int CP_THREADS = 512;                     // 8 waves: one per output block, the rest draw
 // each step's xin / sdw rows are staged in LDS and written as whole float4
 // rows (the MFMA layout gives each lane 4 dims of one path, one column off the
-// 16-byte grid): [xin, sdw][path][CP_SROW] (CP_SROW >= Dp).  One step at a
-// time keeps the workgroup's LDS at 93 KB, so a phase-kernel workgroup (63 KB)
-// still fits beside a prefetched rollout on a CU.
-constexpr int CP_SROW = 148;
-constexpr int CP_STAGE = 2 * CP_PATHS * CP_SROW;
+// 16-byte grid): [xin, sdw][path][SROW] (SROW = 16 nblk + 20 >= Dp).  Two
+// stage buffers: step n's rows are copied out while step n + 1 is computed
+// (one barrier per step; the row stores, bound by the CU's store issue, no
+// longer wait for the MFMA chain and the Euler step, nor they for them).  At
+// nb <= 112 the workgroup's LDS stays at 91 KB, so a phase-kernel workgroup
+// (63 KB) still fits beside a prefetched rollout on a CU.
+__host__ __device__ constexpr int cp_srow(int nblk) { return 16 * nblk + 20; }
+template <int NBLK>
+struct CPGeom {
+  static constexpr int TS = NBLK <= 7 ? 28 : 36;
+  static constexpr int BUF = 4 * 4 * CP_PATHS * TS;     // floats per 4-step draw buffer
+  static constexpr int SROW = cp_srow(NBLK);
+  static constexpr int STAGE = 2 * CP_PATHS * SROW;     // floats per stage buffer
+};
 
 typedef float cpf4 __attribute__((ext_vector_type(4)));
 
 // the uncorrelated sqrt(dt) z of step block sb (steps 4 sb .. 4 sb + 3) of the
 // workgroup's 16 paths into one LDS buffer: item (path, dim) -> 4 steps
+template <int TS>
 __device__ __forceinline__ void corr_draw(const RolloutArgs& p, int m0, int nt4, float sqdt, int sb, float* xb) {
   for (int it = threadIdx.x; it < CP_PATHS * 4 * nt4; it += CP_THREADS) {
     const int pp = it & (CP_PATHS - 1), d = it >> 4;
@@ -397,15 +412,32 @@ __device__ __forceinline__ void corr_draw(const RolloutArgs& p, int m0, int nt4,
     if (d < p.nb && m < p.M) philox_normal4(p.seed, p.offset, (uint32_t)(p.path0 + m), (uint32_t)sb, (uint32_t)d, z);
     const int qq = d & 3, t = d >> 2;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) xb[((k * 4 + qq) * CP_PATHS + pp) * CP_TS + t] = sqdt * z[k];
+    for (int k = 0; k < 4; ++k) xb[((k * 4 + qq) * CP_PATHS + pp) * TS + t] = sqdt * z[k];
+  }
+}
+
+// rows of step n (stage buffer sg) -> xin / sdw: every thread of the
+// workgroup, whole float4 columns
+template <int SROW>
+__device__ __forceinline__ void corr_rows_out(const RolloutArgs& p, const float* sg, int m0, int n, int N1) {
+  if constexpr (DBSDE_AB_CORR & 1) return;
+  const int c4 = p.ldx / 4;
+  for (int it = threadIdx.x; it < 2 * CP_PATHS * c4; it += CP_THREADS) {
+    const int c = it % c4, rest = it / c4, pp = rest % CP_PATHS, arr = rest / CP_PATHS;
+    const int mm = m0 + pp;
+    if (mm >= p.M) continue;
+    const size_t r2 = (size_t)mm * N1 + n;
+    float* dst = arr ? p.sdw : p.xin;
+    *(cpf4*)(dst + r2 * p.ldx + 4 * c) = *(const cpf4*)(sg + (arr * CP_PATHS + pp) * SROW + 4 * c);
   }
 }
 
 // one wave's share: output blocks O1 and O2 (O2 < 0: none; O1 < 0: the wave
 // only draws), K-steps t < 4 O + 4 (the lower triangle; L is zero-padded past
 // nb), everything compile-time so the L fragments stay in registers
-template <int O1, int O2>
+template <int NBLK, int O1, int O2>
 __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs, float* stg) {
+  using G = CPGeom<NBLK>;
   constexpr int NO = (O1 >= 0) + (O2 >= 0);
   constexpr int T1 = O1 >= 0 ? 4 * O1 + 4 : 0, T2 = O2 >= 0 ? 4 * O2 + 4 : 0;
   constexpr int TM = T1 > T2 ? T1 : T2;
@@ -446,21 +478,21 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs, float
   double tacc = 0.0;
   // the K-steps past nb (t >= nt4 up to 4 O + 4) read slots no draw writes:
   // zero both buffers once (0 * stale LDS could be NaN)
-  for (int i = threadIdx.x; i < 2 * CP_BUF; i += CP_THREADS) xs[i] = 0.f;
-  for (int i = threadIdx.x; i < CP_STAGE; i += CP_THREADS) stg[i] = 0.f;   // columns never written stay 0
+  for (int i = threadIdx.x; i < 2 * G::BUF; i += CP_THREADS) xs[i] = 0.f;
+  for (int i = threadIdx.x; i < 2 * G::STAGE; i += CP_THREADS) stg[i] = 0.f;   // columns never written stay 0
   __syncthreads();
-  corr_draw(p, m0, nt4, sqdt, 0, xs);
+  corr_draw<G::TS>(p, m0, nt4, sqdt, 0, xs);
   __syncthreads();
   for (int sb = 0; sb < nsb; ++sb) {
-    if (sb + 1 < nsb) corr_draw(p, m0, nt4, sqdt, sb + 1, xs + ((sb + 1) & 1) * CP_BUF);
-    const float* xb = xs + (sb & 1) * CP_BUF;
+    if (!(DBSDE_AB_CORR & 2) && sb + 1 < nsb) corr_draw<G::TS>(p, m0, nt4, sqdt, sb + 1, xs + ((sb + 1) & 1) * G::BUF);
+    const float* xb = xs + (sb & 1) * G::BUF;
     for (int k = 0; k < 4; ++k) {
       const int n = 4 * sb + k;
       if (n >= p.N) break;
       tacc += dt64;
       const float t1 = (p.t && ok) ? p.t[(size_t)m * N1 + n + 1] : (float)tacc;
       if constexpr (NO > 0) {
-        const float* xr = xb + ((k * 4 + q) * CP_PATHS + cl) * CP_TS;
+        const float* xr = xb + ((k * 4 + q) * CP_PATHS + cl) * G::TS;
         // two independent accumulation chains per block (even / odd K-steps):
         // the dependent-accumulator latency, not the issue rate, bounds a step
         cpf4 acc[2], acc2[2];
@@ -474,6 +506,10 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs, float
             const int t = 4 * s4 + j;
             cpf4& a1 = (j & 1) ? acc2[0] : acc[0];
             cpf4& a2 = (j & 1) ? acc2[1] : acc[1];
+            if constexpr (DBSDE_AB_CORR & 4) {
+              if (t == 0) a1[0] += bz[j];
+              continue;
+            }
             if (t < T1) a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(la1[t < T1 ? t : 0], bz[j], a1, 0, 0, 0);
             if (t < T2) a2 = __builtin_amdgcn_mfma_f32_16x16x4f32(la2[t < T2 ? t : 0], bz[j], a2, 0, 0, 0);
           }
@@ -493,38 +529,33 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs, float
               fa[oc][r].put(p, m, d, n + 1, t1, dw);
               continue;
             }
-            float* sr = stg + cl * CP_SROW;
+            float* sr = stg + (n & 1) * G::STAGE + cl * G::SROW;
             sr[1 + d] = x[oc][r];
             const float sg = rn_add(rn_mul(p.sig_a, x[oc][r]), p.sig_b);
             const float sv = rn_mul(sg, dw);
-            sr[CP_PATHS * CP_SROW + 1 + d] = sv;
+            sr[CP_PATHS * G::SROW + 1 + d] = sv;
             x[oc][r] = rn_add(rn_add(x[oc][r], rn_mul(rn_mul(p.mu_a, x[oc][r]), dt)), sv);
           }
         if (writes_t && p.out == PATH_ROLLOUT) {
-          float* sr = stg + cl * CP_SROW;
+          float* sr = stg + (n & 1) * G::STAGE + cl * G::SROW;
           sr[0] = t0;
           sr[p.D + 1] = 1.0f;
         }
         (void)row;
       }
       if (p.out == PATH_ROLLOUT) {
-        // this step's rows: every thread of the workgroup, whole float4 columns
-        __syncthreads();
-        const int c4 = p.ldx / 4;
-        for (int it = threadIdx.x; it < 2 * CP_PATHS * c4; it += CP_THREADS) {
-          const int c = it % c4, rest = it / c4, pp = rest % CP_PATHS, arr = rest / CP_PATHS;
-          const int mm = m0 + pp;
-          if (mm >= p.M) continue;
-          const size_t r2 = (size_t)mm * N1 + n;
-          float* dst = arr ? p.sdw : p.xin;
-          *(cpf4*)(dst + r2 * p.ldx + 4 * c) = *(const cpf4*)(stg + (arr * CP_PATHS + pp) * CP_SROW + 4 * c);
-        }
-        __syncthreads();   // the stage is rewritten by the next step
+        // the previous step's rows (its stage buffer completed before the last
+        // barrier) while this step's stage fills; the barrier then orders this
+        // step's stage before its copy and the copy before the buffer's reuse
+        if (n > 0) corr_rows_out<G::SROW>(p, stg + ((n - 1) & 1) * G::STAGE, m0, n - 1, N1);
+        if constexpr (!(DBSDE_AB_CORR & 8)) __syncthreads();
       }
       t0 = t1;
     }
     __syncthreads();
   }
+  // the last step's rows
+  if (p.out == PATH_ROLLOUT && p.N > 0) corr_rows_out<G::SROW>(p, stg + ((p.N - 1) & 1) * G::STAGE, m0, p.N - 1, N1);
   if constexpr (NO > 0) {
     if (p.out != PATH_ROLLOUT || !ok) return;
     const size_t row = (size_t)m * N1 + p.N;
@@ -547,17 +578,17 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs, float
 // wave w < NBLK owns output block w; all 8 waves draw
 template <int NBLK>
 __global__ void __launch_bounds__(CP_THREADS) rollout_corr_kernel(RolloutArgs p) {
-  __shared__ __attribute__((aligned(16))) float xs[2 * CP_BUF];
-  __shared__ __attribute__((aligned(16))) float stg[CP_STAGE];
+  __shared__ __attribute__((aligned(16))) float xs[2 * CPGeom<NBLK>::BUF];
+  __shared__ __attribute__((aligned(16))) float stg[2 * CPGeom<NBLK>::STAGE];
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: corr_wave<0, -1>(p, xs, stg); break;
-    case 1: corr_wave<(1 < NBLK ? 1 : -1), -1>(p, xs, stg); break;
-    case 2: corr_wave<(2 < NBLK ? 2 : -1), -1>(p, xs, stg); break;
-    case 3: corr_wave<(3 < NBLK ? 3 : -1), -1>(p, xs, stg); break;
-    case 4: corr_wave<(4 < NBLK ? 4 : -1), -1>(p, xs, stg); break;
-    case 5: corr_wave<(5 < NBLK ? 5 : -1), -1>(p, xs, stg); break;
-    case 6: corr_wave<(6 < NBLK ? 6 : -1), -1>(p, xs, stg); break;
-    default: corr_wave<(7 < NBLK ? 7 : -1), -1>(p, xs, stg); break;
+    case 0: corr_wave<NBLK, 0, -1>(p, xs, stg); break;
+    case 1: corr_wave<NBLK, (1 < NBLK ? 1 : -1), -1>(p, xs, stg); break;
+    case 2: corr_wave<NBLK, (2 < NBLK ? 2 : -1), -1>(p, xs, stg); break;
+    case 3: corr_wave<NBLK, (3 < NBLK ? 3 : -1), -1>(p, xs, stg); break;
+    case 4: corr_wave<NBLK, (4 < NBLK ? 4 : -1), -1>(p, xs, stg); break;
+    case 5: corr_wave<NBLK, (5 < NBLK ? 5 : -1), -1>(p, xs, stg); break;
+    case 6: corr_wave<NBLK, (6 < NBLK ? 6 : -1), -1>(p, xs, stg); break;
+    default: corr_wave<NBLK, (7 < NBLK ? 7 : -1), -1>(p, xs, stg); break;
   }
 }
 
