@@ -1487,6 +1487,21 @@ int launch_tnw(dbsde_ctx* c, int R, int Rp, int s0 = 0, int sn = -1, hipStream_t
   }
   a.P = c->tnw_P;
   a.S = c->tnw_S;
+  // the four waves of a workgroup (one CU, one slice, in step) share operand
+  // rows through the CU's cache: group 0 = {x-stack 0, x-stack 1, block 1,
+  // output}, group g = {x-stack 2g, 2g + 1, blocks 2g, 2g + 1} -- x / zbar
+  // twice and alpha_j / delta_j of each block with its x-stack level
+  for (int g = 0; g < a.P / 4; ++g) {
+    int* o = a.order + 4 * g;
+    if (g == 0) {
+      o[0] = 0; o[1] = 1; o[2] = K + 1; o[3] = a.P - 1;
+    } else {
+      o[0] = 2 * g; o[1] = 2 * g + 1; o[2] = K + 2 * g; o[3] = K + 2 * g + 1;
+    }
+  }
+  if (const char* e = getenv("DBSDE_TNW_ORDER"))   // A/B: 0 = problems in index order
+    if (e[0] == '0')
+      for (int q = 0; q < a.P; ++q) a.order[q] = q;
   a.s0 = s0;
   a.sn = sn < 0 ? a.S : sn;
   a.nchunk = Rp / 16;

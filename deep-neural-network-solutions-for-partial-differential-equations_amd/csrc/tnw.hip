@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(256, 1) tnw_kernel(TNWArgs a) {
   const int wg = blockIdx.x, wpg = a.P / 4;
   const int xcd = wg & 7, local = wg >> 3;
   const int s = a.s0 + (local / wpg) * 8 + xcd;
-  const int p = (local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6);
+  const int p = a.order[(local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6)];
   const TNWProb& pr = a.prob[p];
   const int lane = threadIdx.x & 63, i = lane & 15, kq = lane >> 4;
   const int c0 = (int)((long long)s * a.nchunk / a.S), c1 = (int)((long long)(s + 1) * a.nchunk / a.S);

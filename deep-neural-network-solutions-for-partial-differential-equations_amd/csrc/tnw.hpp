@@ -37,6 +37,7 @@ struct TNWProb {
 struct TNWArgs {
   TNWProb prob[TNW_PMAX];
   int P;          // problems: 2K+1 weight blocks + the output layer (last)
+  int order[TNW_PMAX + 3];   // problem of workgroup slot 4 g + wave (launch_tnw: operand-sharing groups)
   int S;          // row slices per problem (multiple of 8)
   int s0, sn;     // this launch: slices [s0, s0 + sn) (sn multiple of 8; sn = S for the whole reduction)
   int nchunk;     // Rp / 16

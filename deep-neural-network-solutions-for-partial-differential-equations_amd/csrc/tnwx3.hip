@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(256, 1) tnw_x3_kernel(TNWArgs a) {
   const int xcd = wg & 7, local = wg >> 3;
   const int s = a.s0 + (local / wpg) * 8 + xcd;
   // wave-uniform problem index (its operand pointers go to SGPR buffer descriptors)
-  const int p = __builtin_amdgcn_readfirstlane((local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6));
+  const int p = __builtin_amdgcn_readfirstlane(a.order[(local - (local / wpg) * wpg) * 4 + (threadIdx.x >> 6)]);
   const TNWProb& pr = a.prob[p];
   const int lane = threadIdx.x & 63, i = lane & 15, q = lane >> 4;
   const int n32 = a.nchunk / 2;
