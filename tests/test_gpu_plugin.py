@@ -189,3 +189,24 @@ def test_generic_device_step(pkg, dev):
     assert not torch.equal(p0, m.params)
     for it in range(3):
         assert np.isfinite(float(m.device_step(opt, 1e-3, seed=6 + it)))
+
+
+@pytest.mark.parametrize("Dg,mode,act", [(1, "Naisnet", "Sine"), (8, "FC", "Tanh"), (8, "Resnet", "Tanh"),
+                                         (8, "NAIS-Net", "ReLU")])
+def test_custom_problem_other_shapes_match_oracle(pkg, dev, Dg, mode, act):
+    """The generic path at D = 1 (the reference's squeeze() broadcast of the
+    Y-tilde term, DeepBSDE.py:232-233 / SURVEY Q1) and on the other network
+    modes: loss, X / Y / Z and the gradient against the oracle's autograd."""
+    layers = [Dg + 1, 16, 16, 16, 16, 1]
+    xi = np.random.RandomState(9).uniform(0.5, 1.5, (1, Dg)).astype(np.float32)
+    torch.manual_seed(23)
+    m = custom_class(pkg)(xi, T, M, N, Dg, None, layers, mode, act, device=dev)
+    assert not m.native_coefficients
+    np.random.seed(24)
+    t, W = fr.fetch_minibatch(M, N, Dg, T)
+    Xi = torch.from_numpy(xi)
+    ref = fr.loss_and_grads(_oracle_model(m, mode), OracleCustom(kind="custom", D=Dg), t, W, Xi, M, Dg)
+    g = torch.empty_like(m.params)
+    out = m._run(t.to(dev), W.to(dev), Xi.to(dev), grad=g, want=("X", "Y", "Z"))
+    torch.cuda.synchronize()
+    _compare(out, g, ref, ref["used"])
