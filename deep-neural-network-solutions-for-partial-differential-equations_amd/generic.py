@@ -196,18 +196,62 @@ def rollout(fb, t, W, X0):
     return torch.stack(Xs, dim=1), sdw
 
 
-def residual_loss(fb, t, X, U, DU, sdw):
+def phi_row_independent(fb, D, device, P=16, seed=4321):
+    """True when the subclass's phi_tf treats its rows independently: the
+    first P/2 rows of one call over P probe rows equal a call over those rows
+    alone.  The reference calls phi_tf once per time step over the M paths;
+    a row-wise phi gives the same rows when called once over all M N rows
+    (residual_loss's batched form).  A phi that couples rows (a mean over the
+    paths, ...) keeps the per-step loop."""
+    g = torch.Generator().manual_seed(seed)
+    t = torch.rand(P, 1, generator=g)
+    X = 0.5 + torch.rand(P, D, generator=g)
+    Y = torch.randn(P, 1, generator=g)
+    Z = torch.randn(P, D, generator=g)
+    t, X, Y, Z = (v.to(device) for v in (t, X, Y, Z))
+    h = P // 2
+    try:
+        with torch.no_grad():
+            full = fb.phi_tf(t, X, Y, Z)
+            half = fb.phi_tf(t[:h], X[:h], Y[:h], Z[:h])
+    except Exception:   # noqa: BLE001 -- anything unusual keeps the reference's loop
+        return False
+    if not (torch.is_tensor(full) and torch.is_tensor(half) and tuple(full.shape) == (P, 1)
+            and tuple(half.shape) == (h, 1)):
+        return False
+    return bool(torch.allclose(full[:h], half, rtol=1e-5, atol=1e-6))
+
+
+def residual_loss(fb, t, X, U, DU, sdw, batched=False):
     """nd_BSPDE_case.py:259-275: the residuals of the Euler step of Y and the
     terminal terms, with U [M, N+1, 1] and DU [M, N+1, D] in place of the
     network's outputs (torch.squeeze() of the reference's Y-tilde term kept:
-    for D == 1 it broadcasts over the paths)."""
+    for D == 1 it broadcasts over the paths).
+
+    batched: phi_tf once over all M N (path, step) rows instead of once per
+    step -- the same per-row values for a row-wise phi (phi_row_independent)
+    at D > 1, where squeeze() is squeeze(-1); the residual sum then runs in
+    one reduction instead of N (a different fp32 summation order).  One
+    forward and one backward of a handful of kernels instead of ~N x 40: the
+    generic step is bound by those launches."""
     N = t.shape[1] - 1
+    M, D = X.shape[0], X.shape[2]
     loss = 0
-    for n in range(N):
-        t0, t1 = t[:, n, :], t[:, n + 1, :]
-        X0, Y0, Z0, Y1 = X[:, n, :], U[:, n, :], DU[:, n, :], U[:, n + 1, :]
-        Y1t = Y0 + fb.phi_tf(t0, X0, Y0, Z0) * (t1 - t0) + torch.sum(Z0 * torch.squeeze(sdw[n]), dim=1, keepdim=True)
-        loss = loss + torch.sum(torch.pow(Y1 - Y1t, 2))
+    if batched and D > 1:
+        R = M * N
+        S = torch.stack([torch.squeeze(s, dim=-1) for s in sdw], dim=1).reshape(R, D)
+        t0, dt = t[:, :N, :].reshape(R, 1), (t[:, 1:, :] - t[:, :N, :]).reshape(R, 1)
+        X0, Y0, Z0 = X[:, :N, :].reshape(R, D), U[:, :N, :].reshape(R, 1), DU[:, :N, :].reshape(R, D)
+        Y1 = U[:, 1:, :].reshape(R, 1)
+        Y1t = Y0 + fb.phi_tf(t0, X0, Y0, Z0) * dt + torch.sum(Z0 * S, dim=1, keepdim=True)
+        loss = torch.sum(torch.pow(Y1 - Y1t, 2))
+    else:
+        for n in range(N):
+            t0, t1 = t[:, n, :], t[:, n + 1, :]
+            X0, Y0, Z0, Y1 = X[:, n, :], U[:, n, :], DU[:, n, :], U[:, n + 1, :]
+            Y1t = Y0 + fb.phi_tf(t0, X0, Y0, Z0) * (t1 - t0) + torch.sum(Z0 * torch.squeeze(sdw[n]), dim=1,
+                                                                          keepdim=True)
+            loss = loss + torch.sum(torch.pow(Y1 - Y1t, 2))
     XN, YN, ZN = X[:, N, :], U[:, N, :], DU[:, N, :]
     loss = loss + torch.sum(torch.pow(YN - fb.g_tf(XN), 2))
     with torch.enable_grad():
@@ -237,8 +281,15 @@ def loss_grad(fb, params, t, W, Xi, grad=None, want=("X", "Y"), loss_out=None):
     fb.solver.net_u(params, trow, xrow, u, du)
     U = u.view(M, N1, 1).detach().requires_grad_(grad is not None)
     DU = du.view(M, N1, D).detach().requires_grad_(grad is not None)
+    batched = D > 1 and getattr(fb, "_phi_rowwise", None)
+    if D > 1 and batched is None:   # probed once per object
+        batched = phi_row_independent(fb, D, dev)
+        try:
+            fb._phi_rowwise = batched
+        except AttributeError:
+            pass
     with torch.enable_grad() if grad is not None else torch.no_grad():
-        loss = residual_loss(fb, t, X, U, DU, sdw)
+        loss = residual_loss(fb, t, X, U, DU, sdw, batched=bool(batched))
         if grad is not None:
             ubar, zbar = torch.autograd.grad(loss, (U, DU), allow_unused=True)
             ubar = torch.zeros_like(U) if ubar is None else ubar
@@ -258,4 +309,4 @@ def loss_grad(fb, params, t, W, Xi, grad=None, want=("X", "Y"), loss_out=None):
 
 
 __all__ = ["spec_functions", "coefficient_mismatches", "state_independence", "loss_grad", "rollout",
-           "residual_loss", "COEFFICIENTS"]
+           "residual_loss", "phi_row_independent", "COEFFICIENTS"]

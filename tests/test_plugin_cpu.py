@@ -239,3 +239,35 @@ def test_stream_order_selection_over_environments():
               "DBSDE_STREAM_ORDER=auto"):
         assert _order(lib, [e]) == 0, e
     assert _order(lib, None) in (0, 1)        # the process environment
+
+
+def test_batched_residual_equals_the_per_step_loop():
+    """generic.residual_loss over all M N rows at once (row-wise phi, D > 1)
+    against the reference's per-step loop: the loss and its cotangents (u, Z)
+    to fp32 summation-order rounding; a phi that couples the paths of a step
+    is detected and keeps the loop."""
+    torch.manual_seed(5)
+    np.random.seed(5)
+    D, M, N = 8, 12, 7
+    prob = CustomProblem(kind="custom", D=D)
+    fb = fake_fb(prob, D)
+    assert gen.phi_row_independent(fb, D, "cpu")
+    t, W = fr.fetch_minibatch(M, N, D, 1.0)
+    Xi = torch.from_numpy(np.random.uniform(0.5, 1.5, (1, D))).float()
+    X, sdw = gen.rollout(fb, t, W, Xi.repeat(M, 1))
+    U = torch.randn(M, N + 1, 1, requires_grad=True)
+    DU = torch.randn(M, N + 1, D, requires_grad=True)
+    l0 = gen.residual_loss(fb, t, X, U, DU, sdw)
+    l1 = gen.residual_loss(fb, t, X, U, DU, sdw, batched=True)
+    assert float(l1) == pytest.approx(float(l0), rel=1e-6)
+    g0 = torch.autograd.grad(l0, (U, DU))
+    g1 = torch.autograd.grad(l1, (U, DU))
+    for a, b in zip(g0, g1):
+        torch.testing.assert_close(b, a, rtol=1e-5, atol=1e-5 * float(a.abs().max()))
+
+    coupled = fake_fb(prob, D)
+    coupled.phi_tf = lambda t, X, Y, Z: 0.05 * Y + 0.1 * torch.sum(Z.mean(0, keepdim=True) * Z, dim=1, keepdim=True)
+    assert not gen.phi_row_independent(coupled, D, "cpu")
+    broken = fake_fb(prob, D)
+    broken.phi_tf = lambda t, X, Y, Z: torch.sum(Y)   # not one value per row
+    assert not gen.phi_row_independent(broken, D, "cpu")
