@@ -575,20 +575,30 @@ __device__ __forceinline__ void corr_wave(const RolloutArgs& p, float* xs, float
   }
 }
 
-// wave w < NBLK owns output block w; all 8 waves draw
+// The output block of wave w (-1: it only draws).  Block o costs 4 o + 4
+// MFMAs per step (the lower triangle), and waves w and w + 4 share a SIMD, so
+// the blocks go in pairs (7 - s, s) of an 8-block triangle to SIMD s (the
+// NBLK blocks are its last NBLK): at NBLK = 7 the SIMDs issue 28 MFMAs per
+// step each instead of 24 / 32 / 40 / 16 with block w on wave w.
+template <int NBLK>
+constexpr int corr_block_of_wave(int w) {
+  const int s = w & 3, v = (w >> 2) ? s : 7 - s, b = v - (8 - NBLK);
+  return b >= 0 ? b : -1;
+}
+// all 8 waves draw
 template <int NBLK>
 __global__ void __launch_bounds__(CP_THREADS) rollout_corr_kernel(RolloutArgs p) {
   __shared__ __attribute__((aligned(16))) float xs[2 * CPGeom<NBLK>::BUF];
   __shared__ __attribute__((aligned(16))) float stg[2 * CPGeom<NBLK>::STAGE];
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {
-    case 0: corr_wave<NBLK, 0, -1>(p, xs, stg); break;
-    case 1: corr_wave<NBLK, (1 < NBLK ? 1 : -1), -1>(p, xs, stg); break;
-    case 2: corr_wave<NBLK, (2 < NBLK ? 2 : -1), -1>(p, xs, stg); break;
-    case 3: corr_wave<NBLK, (3 < NBLK ? 3 : -1), -1>(p, xs, stg); break;
-    case 4: corr_wave<NBLK, (4 < NBLK ? 4 : -1), -1>(p, xs, stg); break;
-    case 5: corr_wave<NBLK, (5 < NBLK ? 5 : -1), -1>(p, xs, stg); break;
-    case 6: corr_wave<NBLK, (6 < NBLK ? 6 : -1), -1>(p, xs, stg); break;
-    default: corr_wave<NBLK, (7 < NBLK ? 7 : -1), -1>(p, xs, stg); break;
+    case 0: corr_wave<NBLK, corr_block_of_wave<NBLK>(0), -1>(p, xs, stg); break;
+    case 1: corr_wave<NBLK, corr_block_of_wave<NBLK>(1), -1>(p, xs, stg); break;
+    case 2: corr_wave<NBLK, corr_block_of_wave<NBLK>(2), -1>(p, xs, stg); break;
+    case 3: corr_wave<NBLK, corr_block_of_wave<NBLK>(3), -1>(p, xs, stg); break;
+    case 4: corr_wave<NBLK, corr_block_of_wave<NBLK>(4), -1>(p, xs, stg); break;
+    case 5: corr_wave<NBLK, corr_block_of_wave<NBLK>(5), -1>(p, xs, stg); break;
+    case 6: corr_wave<NBLK, corr_block_of_wave<NBLK>(6), -1>(p, xs, stg); break;
+    default: corr_wave<NBLK, corr_block_of_wave<NBLK>(7), -1>(p, xs, stg); break;
   }
 }
 
