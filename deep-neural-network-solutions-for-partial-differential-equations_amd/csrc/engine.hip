@@ -34,9 +34,12 @@
 #ifndef DBSDE_DEFER_PF
 #define DBSDE_DEFER_PF 1
 #endif
-// device-mode diagonal rollout with the draws spread over the time steps
-// (rollout_steps_kernel, 1) or one thread per (path, column group) for all
-// steps (rollout4_kernel, 0).  The prefetched rollout is off the step's
+// device-mode diagonal rollout: in-step by default the two-pass form (parallel
+// draws into the sdw rows, then the Euler chains: rollout_draw_kernel +
+// rollout_chain_kernel, ctx rollout2; DBSDE_ROLLOUT2=0 turns it off: M = 128
+// 0.146 vs 0.156 ms/step, profiles/r6_ab_rollout.txt 4); prefetched, and else, the
+// draws spread over the time steps (rollout_steps_kernel, DBSDE_RS = 1) or one
+// thread per (path, column group) for all steps (rollout4_kernel, 0).  The prefetched rollout is off the step's
 // critical path either way (0.4472 vs 0.4445 ms/step at M = 1024, 0.140 vs
 // 0.140 at M = 128), but beside the phase section of a profiled step the
 // step-parallel kernel's 4-wave, 32 KB-LDS workgroups slow the section by
@@ -229,6 +232,7 @@ struct dbsde_ctx {
   int tnw_nb = 0, tnw_P = 0, tnw_S = 128;  // P * S = 1024 waves = one per SIMD at K = 3
   int tnw_Smax = 128;                       // slab capacity; tnw_S is set per batch (tnw_slices)
   bool tnw_x3 = false;                     // split-bf16 weight-gradient kernel (tnwx3.hip)
+  bool rollout2 = true;                    // two-pass device-mode diagonal rollout (paths.hpp)
   float* slabW = nullptr;
   int fin_blocks = 1;             // slabsum grid.x
 
@@ -750,6 +754,7 @@ int build_buffers(dbsde_ctx* c) {
   // P = 2K + 2 problems in 4-wave workgroups: K odd
   c->tnw = c->has_v && uniformW && c->Wp[0] == Dp && Dp <= 128 && K <= 6 && (2 * K + 2) % 4 == 0;
   if (const char* e = getenv("DBSDE_TNW")) c->tnw = c->tnw && atoi(e) != 0;
+  if (const char* e = getenv("DBSDE_ROLLOUT2")) c->rollout2 = atoi(e) != 0;
   std::vector<PackDesc> F;
   if (c->tnw) {
     const int T = Dp, P = 2 * K + 2, S = c->tnw_Smax;
@@ -1042,7 +1047,10 @@ void launch_corr(const RolloutArgs& ra, hipStream_t s) {
 
 // Euler-Maruyama paths (ra.out == PATH_ROLLOUT) or the device fetch_minibatch
 // (PATH_FETCH_*): Heston, Cholesky-correlated device mode, or diagonal
-int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
+// side: a prefetched rollout running beside other work (the two-pass form's
+// 1456-workgroup draw pass floods the CUs the phase section runs on: 0.451 vs
+// 0.443 ms/step prefetched at M = 1024, so it serves in-step rollouts only)
+int launch_paths(dbsde_ctx* c, RolloutArgs& ra, bool side = false) {
   hipStream_t s = c->stream;
   const char* name = ra.out == PATH_ROLLOUT ? "rollout" : "brownian";
   const double steps = (double)ra.M * ra.N;
@@ -1055,6 +1063,13 @@ int launch_paths(dbsde_ctx* c, RolloutArgs& ra) {
       return fail(c, DBSDE_EINVAL, "internal: correlated rollout row staging");
     RUN(c, name, 2.0 * steps * ra.nb * ra.nb / 2, bytes,
         launch_corr(ra, s));
+  } else if (c->rollout2 && !side && ra.out == PATH_ROLLOUT && !ra.W && !ra.t && ra.ldx % 4 == 0) {
+    // device-mode increments: parallel draws, then the Euler chains (paths.hpp)
+    const long long draws = (long long)ra.M * ((ra.N + 3) / 4) * (ra.ldx / 4);
+    const int chains = ra.M * (ra.ldx / 4);
+    RUN(c, name, 0.0, bytes,
+        rollout_draw_kernel<<<(unsigned)((draws + 255) / 256), 256, 0, s>>>(ra);
+        rollout_chain_kernel<<<(unsigned)((chains + RC_THREADS - 1) / RC_THREADS), RC_THREADS, 0, s>>>(ra));
   } else if (DBSDE_RS && ra.out == PATH_ROLLOUT && !ra.W && ra.ldx % 4 == 0) {
     // device-mode increments: draws spread over the time steps (paths.hpp)
     const long long pairs = (long long)ra.M * (ra.ldx / 4);
@@ -1095,7 +1110,7 @@ int issue_prefetch(dbsde_ctx* c, const dbsde_batch* next, const float* avoid = n
   if (e == hipSuccess) {
     RolloutArgs ra = rollout_args(c, next);
     ra.out = PATH_ROLLOUT;
-    rc = launch_paths(c, ra);
+    rc = launch_paths(c, ra, true);
   }
   c->stream = main_stream;
   c->xin = xin0;
@@ -1143,7 +1158,7 @@ int launch_deferred_on(dbsde_ctx* c, hipStream_t st) {
   if (e == hipSuccess) {
     RolloutArgs ra = rollout_args(c, &nb);
     ra.out = PATH_ROLLOUT;
-    rc = launch_paths(c, ra);
+    rc = launch_paths(c, ra, true);
   }
   c->stream = main_stream;
   c->xin = xin0;

@@ -354,6 +354,108 @@ __global__ void __launch_bounds__(RS_THREADS) rollout_steps_kernel(RolloutArgs p
 }
 
 // --------------------------------------------------------------------------
+// Device-mode diagonal rollout in two passes (the default for device-mode
+// diagonal problems).  rollout4_kernel's 28 M threads each run Philox +
+// Box-Muller + Euler for all N steps in sequence, so the draws sit on the
+// chain and only M / 9 workgroups exist (33 us at M = 128 as at M = 1024).
+//   pass 1 (rollout_draw_kernel): every (path, 4-step Philox block, 16-byte
+//     column group) draws in parallel and writes the raw increments
+//     sqrt(dt) z into the sdw rows (columns of dims outside [0, D) are 0);
+//   pass 2 (rollout_chain_kernel): thread per (path, column group), 64-thread
+//     workgroups (spread over every CU: the row stores are bound by each CU's
+//     store issue), runs the Euler recursion reading its increments 8 steps
+//     ahead and overwrites each sdw row in place with sigma(X) dW.
+// Per dimension every value is rollout4_kernel's (same Philox key, same
+// sqrt(dt) z, same non-contracted step, the same sequential fp64 time grid),
+// so X is bit-identical; sdw is read once more and written once more (2 x
+// 4 M N Dp bytes).
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) rollout_draw_kernel(RolloutArgs p) {
+  const int C = p.ldx >> 2, nsb = (p.N + 3) >> 2;
+  const long long gid = blockIdx.x * 256LL + threadIdx.x;
+  if (gid >= (long long)p.M * nsb * C) return;
+  const int c = (int)(gid % C);
+  const long long rest = gid / C;
+  const int b = (int)(rest % nsb), m = (int)(rest / nsb);
+  const float sqdt = sqrtf(p.T / (float)p.N);
+  float dw[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int d = 4 * c + k - 1;
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    if (d >= 0 && d < p.D) philox_normal4(p.seed, p.offset, (uint32_t)(p.path0 + m), (uint32_t)b, (uint32_t)d, z);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) dw[k][s2] = (d >= 0 && d < p.D) ? sqdt * z[s2] : 0.f;
+  }
+  const size_t r0 = (size_t)m * (p.N + 1) + 4 * b;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2)
+    if (4 * b + s2 < p.N)
+      *(floatx4*)(p.sdw + (r0 + s2) * p.ldx + 4 * c) = floatx4{dw[0][s2], dw[1][s2], dw[2][s2], dw[3][s2]};
+}
+
+constexpr int RC_THREADS = 64;
+constexpr int RC_AHEAD = 8;   // increments loaded ahead of the chain
+__global__ void __launch_bounds__(RC_THREADS) rollout_chain_kernel(RolloutArgs p) {
+  const int C = p.ldx >> 2;
+  const int gid = blockIdx.x * RC_THREADS + threadIdx.x;
+  if (gid >= p.M * C) return;
+  const int m = gid / C, c = gid - m * C;
+  const int N1 = p.N + 1;
+  float x[4];
+  bool live[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int d = 4 * c + k - 1;
+    live[k] = d >= 0 && d < p.D;
+    x[k] = live[k] ? p.Xi[(p.xi_rows == 1 ? 0 : m) * p.D + d] : 0.f;
+  }
+  const double dt64 = (double)p.T / (double)p.N;
+  double tacc = 0.0;
+  float t0 = 0.0f;
+  const size_t r0 = (size_t)m * N1;
+  for (int n0 = 0; n0 < p.N; n0 += RC_AHEAD) {
+    floatx4 dw[RC_AHEAD];
+#pragma unroll
+    for (int i = 0; i < RC_AHEAD; ++i)
+      dw[i] = n0 + i < p.N ? *(const floatx4*)(p.sdw + (r0 + n0 + i) * p.ldx + 4 * c) : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < RC_AHEAD; ++i) {
+      const int n = n0 + i;
+      if (n >= p.N) break;
+      tacc += dt64;
+      const float t1 = (float)tacc;
+      const float dt = rn_sub(t1, t0);
+      floatx4 xo, so;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int col = 4 * c + k;
+        float sv = 0.f;
+        if (live[k]) {
+          const float sg = rn_add(rn_mul(p.sig_a, x[k]), p.sig_b);
+          sv = rn_mul(sg, dw[i][k]);
+        }
+        xo[k] = col == 0 ? t0 : (col == p.D + 1 ? 1.f : x[k]);
+        so[k] = sv;
+        if (live[k]) x[k] = rn_add(rn_add(x[k], rn_mul(rn_mul(p.mu_a, x[k]), dt)), sv);
+      }
+      *(floatx4*)(p.xin + (r0 + n) * p.ldx + 4 * c) = xo;
+      *(floatx4*)(p.sdw + (r0 + n) * p.ldx + 4 * c) = so;
+      t0 = t1;
+    }
+  }
+  floatx4 xo, so;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {   // n = N
+    const int col = 4 * c + k;
+    xo[k] = col == 0 ? t0 : (col == p.D + 1 ? 1.f : x[k]);
+    so[k] = 0.f;
+  }
+  *(floatx4*)(p.xin + (r0 + p.N) * p.ldx + 4 * c) = xo;
+  *(floatx4*)(p.sdw + (r0 + p.N) * p.ldx + 4 * c) = so;
+}
+
+// --------------------------------------------------------------------------
 // Cholesky-correlated device mode (with_corr...py:339-341: dW = L (sqrt(dt) z))
 // with the correlation product on the matrix cores: per step n the increments
 // of a 16-path group are dW^T = L . xi^T, one v_mfma_f32_16x16x4_f32 per

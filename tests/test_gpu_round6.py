@@ -97,3 +97,34 @@ def test_prefetch_consumed_on_another_stream(pkg, dev, g):
     swapped = _run_steps(_model(pkg, dev, g), seeds, lambda i: seeds[i + 1] if i + 1 < len(seeds) else None,
                          streams=[s1, s2])
     _same(swapped, base)
+
+
+@pytest.mark.parametrize("Mr,Nr,D", [(1024, 50, 100), (37, 13, 100), (5, 3, 7)])
+def test_two_pass_rollout_equals_single_pass(pkg, dev, monkeypatch, Mr, Nr, D):
+    """The in-step device rollout in two passes (rollout_draw_kernel +
+    rollout_chain_kernel, paths.hpp) against rollout4_kernel
+    (DBSDE_ROLLOUT2=0, read at context creation): X, Y, Z, loss and gradient
+    bit for bit, also at ragged M and at N not a multiple of the 4-step Philox
+    block or the 8-step load-ahead."""
+    layers = [D + 1, 16, 16, 16, 16, 1]
+    xi = np.random.RandomState(3).uniform(0.5, 1.5, (1, D)).astype(np.float32)
+
+    def run(flag):
+        if flag is None:
+            monkeypatch.delenv("DBSDE_ROLLOUT2", raising=False)
+        else:
+            monkeypatch.setenv("DBSDE_ROLLOUT2", flag)
+        torch.manual_seed(4)
+        m = pkg.BlackScholesBarenblatt(xi, 1.0, Mr, Nr, D, layers, "NAIS-Net", "Sine", device=dev)
+        o = dict(loss=torch.empty(1, device=dev), X=torch.empty(Mr * (Nr + 1) * D, device=dev),
+                 Y=torch.empty(Mr * (Nr + 1), device=dev), Z=torch.empty(Mr * (Nr + 1) * D, device=dev),
+                 grad=torch.empty_like(m.params))
+        m.solver.loss_grad(m.params, Mr, Nr, m._device_xi(0, Mr), seed=77, grad=o["grad"], loss=o["loss"], X=o["X"],
+                           Y=o["Y"], Z=o["Z"])
+        torch.cuda.synchronize()
+        return {k: v.cpu() for k, v in o.items()}
+
+    two, one = run(None), run("0")
+    assert torch.isfinite(two["X"]).all()
+    for k in two:
+        torch.testing.assert_close(two[k], one[k], rtol=0, atol=0, msg=k)
