@@ -128,3 +128,32 @@ def test_two_pass_rollout_equals_single_pass(pkg, dev, monkeypatch, Mr, Nr, D):
     assert torch.isfinite(two["X"]).all()
     for k in two:
         torch.testing.assert_close(two[k], one[k], rtol=0, atol=0, msg=k)
+
+
+def test_large_batch_is_the_sum_of_its_halves(pkg, dev, g):
+    """M = 16384 paths per GPU (16x the north star: R = 835,584 rows, 13,056
+    phase workgroups per launch, the two-chunk pipeline with prefetch-free
+    in-step rollouts) against its two halves, drawn with the device Philox
+    keyed by the global path index (path0 = 0 and 8192): X bit for bit, the
+    loss and the gradient as sums over the paths (DeepBSDE.py:231-241)."""
+    Ml, Nl = 16384, 50
+    m = _model(pkg, dev, g)
+    D = m.state_dim
+    xi = m._device_xi(0, M)
+
+    def run(M, path0):
+        o = dict(loss=torch.empty(1, device=dev), X=torch.empty(M * (Nl + 1) * D, device=dev),
+                 Y=torch.empty(M * (Nl + 1), device=dev), grad=torch.empty_like(m.params))
+        m.solver.loss_grad(m.params, M, Nl, xi, seed=99, path0=path0, grad=o["grad"], loss=o["loss"], X=o["X"],
+                           Y=o["Y"])
+        torch.cuda.synchronize()
+        return {k: v.cpu().double() for k, v in o.items()}
+
+    full = run(Ml, 0)
+    a, b = run(Ml // 2, 0), run(Ml // 2, Ml // 2)
+    assert torch.isfinite(full["loss"]).all() and torch.isfinite(full["grad"]).all()
+    torch.testing.assert_close(full["X"], torch.cat([a["X"], b["X"]]), rtol=0, atol=0)
+    torch.testing.assert_close(full["Y"], torch.cat([a["Y"], b["Y"]]), rtol=0, atol=1e-5 * float(full["Y"].abs().max()))
+    assert float(full["loss"]) == pytest.approx(float(a["loss"] + b["loss"]), rel=1e-5)
+    g2 = a["grad"] + b["grad"]
+    torch.testing.assert_close(full["grad"], g2, rtol=0, atol=2e-5 * float(g2.abs().max()))
