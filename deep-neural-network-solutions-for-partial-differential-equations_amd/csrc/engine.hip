@@ -1133,9 +1133,11 @@ int flush_deferred(dbsde_ctx* c, const float* avoid = nullptr) {
   return issue_prefetch(c, &b, avoid);
 }
 // the held-back prefetch on stream st (the chunked step's second stream, after
-// its weight-gradient slices), into the path buffer the current step does not
-// use; its pending entry is joined (the join write follows on st).  Falls back
-// to pf_stream when no buffer is free.
+// its weight-gradient slices and its join into the main stream), into the path
+// buffer the current step does not use: it runs beside the step's tail
+// (finalize, projection adjoint, repack: a few latency-bound workgroups) and
+// only the next step's phase A waits for it (its ready mark, wait_pending).
+// Falls back to pf_stream when no buffer is free.
 int launch_deferred_on(dbsde_ctx* c, hipStream_t st) {
   if (!c->deferred) return DBSDE_OK;
   int j = -1;
@@ -1165,9 +1167,9 @@ int launch_deferred_on(dbsde_ctx* c, hipStream_t st) {
   c->sdw = sdw0;
   if (e != hipSuccess) return fail(c, DBSDE_EHIP, std::string("prefetch: ") + hipGetErrorString(e));
   if (rc) return rc;
+  if ((rc = order_mark(c, ORD_PEND0 + j, st, c->pend[j].ready_v))) return rc;
   c->pend[j].valid = true;
-  c->pend[j].joined = true;
-  c->pend[j].joined_to = c->stream;
+  c->pend[j].joined = false;
   c->pend[j].b = nb;
   c->pend[j].seq = ++c->pf_seq;
   return DBSDE_OK;
@@ -2337,11 +2339,9 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
         t0 += tiles;
       }
       HIPC(c, hipGetLastError());
-      if ((tnw_piped || tn_piped) && (rc = launch_deferred_on(c, c->pipe2))) return rc;
-      // the pending prefetched rollouts (the next step's paths, started a step
-      // ago) are waited for on the second chunk stream, which finishes ahead of
-      // the main one, so the join orders the main stream after them too and
-      // the next step's phase A needs no wait of its own
+      // the pending prefetched rollouts (this step's other buffer, started a
+      // step ago) are waited for on the second chunk stream, so the join orders
+      // the main stream after them too
       for (int i = 0; i < 2; ++i)
         if (c->pend[i].valid) {
           // (a rollout joined before is already behind pipe2: the join below
@@ -2351,6 +2351,9 @@ int loss_grad_impl(dbsde_ctx* c, const float* params, const dbsde_batch* b, floa
           c->pend[i].joined_to = s;
         }
       if ((rc = stream_order(c, c->pipe2, s, ORD_JOIN))) return rc;
+      // the held-back batch after the join: beside this step's tail, not in
+      // front of it (profiles/r6_ab_rollout.txt 6)
+      if ((tnw_piped || tn_piped) && (rc = launch_deferred_on(c, c->pipe2))) return rc;
       if (c->prof) {
         HIPC(c, hipEventRecord(c->ev_prof[1], s));
         HIPC(c, hipEventSynchronize(c->ev_prof[1]));
