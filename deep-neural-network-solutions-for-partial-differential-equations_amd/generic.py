@@ -185,14 +185,17 @@ def rollout(fb, t, W, X0):
     Y0 = torch.zeros((M, 1), device=X0.device)
     Z0 = torch.zeros((M, D), device=X0.device)
     Xs, sdw = [X0], []
-    t0, W0 = t[:, 0, :], W[:, 0, :]
+    # the increments and time steps of every step at once: the same
+    # element-wise fp32 differences the per-step W1 - W0 / t1 - t0 take
+    dW = (W[:, 1:, :] - W[:, :-1, :]).unsqueeze(-1)
+    dt = t[:, 1:, :] - t[:, :-1, :]
     for n in range(N1 - 1):
-        t1, W1 = t[:, n + 1, :], W[:, n + 1, :]
-        s = torch.matmul(fb.sigma_tf(t0, X0, Y0), (W1 - W0).unsqueeze(-1))
-        X1 = X0 + fb.mu_tf(t0, X0, Y0, Z0) * (t1 - t0) + torch.squeeze(s, dim=-1)
+        t0 = t[:, n, :]
+        s = torch.matmul(fb.sigma_tf(t0, X0, Y0), dW[:, n])
+        X1 = X0 + fb.mu_tf(t0, X0, Y0, Z0) * dt[:, n] + torch.squeeze(s, dim=-1)
         sdw.append(s)
         Xs.append(X1)
-        t0, W0, X0 = t1, W1, X1
+        X0 = X1
     return torch.stack(Xs, dim=1), sdw
 
 
